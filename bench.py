@@ -1,0 +1,214 @@
+#!/usr/bin/env python3
+"""Benchmark: device-resident ChaCha20-Poly1305 seal+open over 16 KiB TLS records.
+
+Metric (BASELINE.json): "GiB/s device-resident ChaCha20-Poly1305 over 16 KiB TLS
+records, 1/2/4/8 GPUs".  One step = seal every record of the shard, then open
+every sealed record (C1 of BASELINE.json: 2^20 x 16 KiB per GPU, one key,
+sequential sequence numbers, TLS nonce/AD built on device).  value = plaintext
+bytes processed by seal and open on all ranks / wall time of the timed region
+(max over ranks), in GiB/s.  Weak scaling: each rank owns its own 2^20 records
+(seq r*2^20 + i); there is no collective in the data path.
+
+Usage:  python bench.py [--gpus N] [--steps K] [--warmup W]
+        torchrun --nproc-per-node N bench.py --gpus N ...   (N > 1)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak, /opt/skills/guides/MI355X_MICROARCH.md
+SEED = 0x53555255
+KEY = bytes(range(32))
+METRIC = "GiB/s device-resident ChaCha20-Poly1305 over 16 KiB TLS records, 1/2/4/8 GPUs"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--records", type=int, default=1 << 20, help="records per GPU (C1: 2^20)")
+    ap.add_argument("--record-bytes", type=int, default=16384)
+    ap.add_argument("--cpu-sample", type=int, default=4096, help="records in the CPU-baseline sample")
+    ap.add_argument("--cpu-seconds", type=float, default=2.0, help="min wall time of the CPU baseline")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic", default=str(ROOT / "profiles" / "traffic_r01.json"),
+                    help="PMC-derived HBM traffic summary (tools/pmc_traffic.py)")
+    return ap.parse_args()
+
+
+def cpu_baseline(args, n):
+    """Oracle (suruga-algorithm C restatement) on the host cores: bounded sample."""
+    sys.path.insert(0, str(ROOT / "tests"))
+    from oracle_ffi import oracle as get_oracle  # checker/baseline only, never the measured path
+
+    o = get_oracle()
+    count = args.cpu_sample
+    threads = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()))
+    pt = b"".join(o.fill_record(SEED, j, n) for j in range(count))
+    reps, t = 0, 0.0
+    while t < args.cpu_seconds:
+        t0 = time.perf_counter()
+        ct = o.seal_batch_tls(KEY, 0, pt, n, count, threads=threads)
+        bad, back, _ = o.open_batch_tls(KEY, 0, ct, n, count, threads=threads)
+        t += time.perf_counter() - t0
+        reps += 1
+        assert bad == 0 and back == pt
+    gibs = 2 * count * n * reps / t / 2**30
+    # single-thread rate on a slice (the reference is single-threaded per connection)
+    c1 = max(64, count // 16)
+    t0 = time.perf_counter()
+    ct1 = o.seal_batch_tls(KEY, 0, pt[:c1 * n], n, c1, threads=1)
+    o.open_batch_tls(KEY, 0, ct1, n, c1, threads=1)
+    t1 = time.perf_counter() - t0
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {
+        "value": round(gibs, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+        "sample": f"{count} x {n} B TLS records seal+open, x{reps} repetitions, {threads} threads "
+                  f"(oracle/suruga_oracle.c, the reference's scalar algorithm)",
+        "single_thread_gibs": round(2 * c1 * n / t1 / 2**30, 4), "cpu": model or platform.processor(),
+    }
+
+
+def main():
+    args = parse()
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    from suruga_amd import _build
+    from suruga_amd import batch as B
+
+    if not _build.LIB.exists():
+        _build.build_library()
+    n, count = args.record_bytes, args.records
+    seq0 = rank * count
+    keys = torch.tensor(list(KEY), dtype=torch.uint8, device=dev).view(1, 32)
+    pt = torch.empty(count * n, dtype=torch.uint8, device=dev)
+    ct = torch.empty(count * (n + 16), dtype=torch.uint8, device=dev)
+    back = torch.empty(count * n, dtype=torch.uint8, device=dev)
+    status = torch.empty(count, dtype=torch.uint8, device=dev)
+    ws = torch.empty(B.workspace_size(count), dtype=torch.uint8, device=dev)
+    B.fill_records(pt, n, n, count, SEED, j0=seq0)
+    stream = torch.cuda.current_stream(dev)
+    seal_b = B.Batch(count=count, keys=keys, inp=pt, out=ct, uniform_len=n, in_stride=n, out_stride=n + 16,
+                     seq0=seq0, workspace=ws, stream=stream)
+    open_b = B.Batch(count=count, keys=keys, inp=ct, out=back, uniform_len=n + 16, in_stride=n + 16,
+                     out_stride=n, seq0=seq0, status=status, workspace=ws, stream=stream)
+    seal_c, open_c = seal_b.to_c(), open_b.to_c()
+    lib = B.N.load()
+    import ctypes as C
+
+    def step():
+        B.N.check(lib.sg_seal_batch(C.byref(seal_c)))
+        B.N.check(lib.sg_open_batch(C.byref(open_c)))
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # correctness of the last step (outside the timed region)
+    mism = torch.zeros(1, dtype=torch.int64, device=dev)
+    B.compare_records(pt, n, back, n, n, count, mism, stream=stream)
+    bad_status = int((status != 0).sum().item())
+    roundtrip_ok = int(mism.item()) == 0 and bad_status == 0
+
+    # per-kernel device time with HIP events on the launch stream
+    B.set_timing(True)
+    for _ in range(3):
+        step()
+    tm = B.timing_read()
+    B.set_timing(False)
+
+    payload = 2 * count * n * args.steps * world  # seal + open plaintext bytes, all ranks
+    value = payload / elapsed / 2**30
+    ms_per_step = elapsed / args.steps * 1e3
+
+    # dominant kernel's roofline (algorithmic bytes per launch):
+    # seal R+W = 2n + 69 per record, open = 2n + 70
+    dom = "open" if tm["open_ms"] >= tm["seal_ms"] else "seal"
+    per_rec = 2 * n + (70 if dom == "open" else 69)
+    alg_bytes = per_rec * count
+    dom_ms = tm[f"{dom}_ms"]
+    achieved = alg_bytes / (dom_ms * 1e-3) / 1e9
+    traffic = None
+    tp = Path(args.traffic)
+    if tp.exists():
+        try:
+            tj = json.loads(tp.read_text())
+            if tj.get("records") == count and tj.get("record_bytes") == n:
+                traffic = tj.get(f"{dom}_bytes_per_launch")
+        except (ValueError, OSError):
+            traffic = None
+
+    if rank == 0:
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(args, n)
+        line = {
+            "metric": METRIC, "value": round(value, 3), "unit": "GiB/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+            "data": "synthetic (splitmix64 records generated on device)",
+            "config": {"workload": f"C1: {count} x {n} B TLS records per GPU, one key, sequential seq, "
+                                   "seal then open, device-resident",
+                       "records_per_gpu": count, "record_bytes": n, "parallelism": f"record-shard x{world}",
+                       "kernels": lib.sg_build_info().decode()},
+            "roofline": {"bound": "hbm", "kernel": f"sg_aead_kernel<{'OPEN' if dom == 'open' else 'SEAL'}>",
+                         "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "alg_bytes_per_launch": alg_bytes, "avg_launch_ms": round(dom_ms, 4)},
+            "kernel_ms": {"seal": round(tm["seal_ms"], 4), "open": round(tm["open_ms"], 4),
+                          "keying": round(tm["keying_ms"], 4)},
+            "correct": roundtrip_ok,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+    if not roundtrip_ok:
+        sys.exit(3)
+
+
+if __name__ == "__main__":
+    main()

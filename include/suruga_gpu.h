@@ -1,0 +1,188 @@
+/*
+ * suruga_gpu.h -- C ABI of the MI355X (gfx950) ChaCha20-Poly1305 record AEAD.
+ *
+ * This is the drop-in boundary for suruga's cipher plugin interface
+ * (klutzy/suruga src/cipher/mod.rs:14-32).  Every entry point below replaces
+ * one item of that interface; the reference-side bindings a maintainer would
+ * add are shown in INTEGRATION.md.
+ *
+ *   Aead::key_size / fixed_iv_len / mac_len      mod.rs:15-17
+ *       -> sg_key_size / sg_fixed_iv_len / sg_mac_len
+ *          (values from chacha20_poly1305.rs:15-17, 102-119)
+ *   Aead::new_encryptor / new_decryptor           mod.rs:18-19, chacha20_poly1305.rs:121-134
+ *       -> sg_ctx_new (one context per direction, key moved in) / sg_ctx_free
+ *   Encryptor::encrypt(nonce, plain, ad) -> Vec   mod.rs:22-24, chacha20_poly1305.rs:48-59
+ *       -> sg_seal   (caller-provided out of n + 16 bytes: ct || tag)
+ *   Decryptor::decrypt(nonce, encrypted, ad)      mod.rs:28-31, chacha20_poly1305.rs:65-94
+ *       -> sg_open   (returns SG_E_BAD_MAC / SG_E_SHORT where the reference
+ *                     returns Err(TlsError{kind: BadRecordMac, ..}))
+ *   Decryptor::mac_len                            mod.rs:31, chacha20_poly1305.rs:96-99
+ *       -> sg_mac_len
+ *   TlsWriter::write_data chunk loop / TlsReader::read_record (tls.rs:99-147,217-281)
+ *       -> sg_seal_batch / sg_open_batch: many records per call, nonce and the
+ *          13-byte additional data built on the device from the record-layer
+ *          rules (tls.rs:103-112, 250-265) in SG_BATCH_TLS mode.
+ *
+ * Construction: draft-agl-tls-chacha20poly1305-04 as implemented by suruga
+ * (64-bit nonce, 32-bit block counter in state word 12 only, Poly1305 key =
+ * keystream block 0, MAC over ad || le64(|ad|) || ct || le64(|ct|) with no
+ * padding).  NOT RFC 7539.
+ *
+ * Plain C types only: no HIP or torch types cross this boundary.  Device
+ * pointers are passed as plain pointers; a HIP stream as void*.
+ */
+#ifndef SURUGA_GPU_H
+#define SURUGA_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SG_ABI_VERSION 1
+
+/* ---- status codes ------------------------------------------------------ */
+#define SG_OK          0
+#define SG_E_BAD_MAC   1   /* tag mismatch: TlsErrorKind::BadRecordMac "wrong mac"
+                              (chacha20_poly1305.rs:89-90)                        */
+#define SG_E_SHORT     2   /* input shorter than the tag: BadRecordMac "message too
+                              short" (chacha20_poly1305.rs:68-70)                 */
+#define SG_E_ARG      -1   /* bad argument (lengths, NULL pointers, limits); the
+                              reference panics here (chacha20.rs:26-27)           */
+#define SG_E_HIP      -2   /* HIP runtime error                                  */
+#define SG_E_NODEV    -3   /* no usable gfx950 device                            */
+
+/* ---- limits ------------------------------------------------------------ */
+#define SG_KEY_LEN         32u
+#define SG_NONCE_LEN        8u
+#define SG_MAC_LEN         16u
+#define SG_MAX_AD_LEN     255u
+/* One record is one workgroup and its ciphertext is staged in LDS for the
+ * MAC.  TLS records are at most 2^14 (+2048 expansion) bytes (tls.rs:32-35). */
+#define SG_MAX_RECORD_LEN 32768u
+
+/* ---- Aead constants (chacha20_poly1305.rs:15-17, 104-119) --------------- */
+size_t sg_key_size(void);     /* 32 */
+size_t sg_fixed_iv_len(void); /* 0  */
+size_t sg_mac_len(void);      /* 16 */
+int    sg_abi_version(void);  /* SG_ABI_VERSION */
+
+/* ---- per-direction context (Aead::new_encryptor / new_decryptor) -------- */
+typedef struct sg_ctx sg_ctx;
+
+/* Copies the 32-byte key to device `device` (HIP ordinal).  Returns NULL on
+ * failure (sg_last_error() says why). */
+sg_ctx* sg_ctx_new(const uint8_t key[32], int device);
+void    sg_ctx_free(sg_ctx* ctx);
+
+/* Encryptor::encrypt.  Host pointers.  out receives n + 16 bytes (ct || tag).
+ * nonce is 8 bytes (TLS: be64(seq), tls.rs:103).  Returns SG_OK or < 0. */
+int sg_seal(sg_ctx* ctx, const uint8_t* nonce, size_t nonce_len,
+            const uint8_t* pt, size_t n, const uint8_t* ad, size_t adlen, uint8_t* out);
+
+/* Decryptor::decrypt.  Host pointers.  in = ct || tag (in_len bytes); out
+ * receives in_len - 16 bytes of plaintext on SG_OK.  On SG_E_BAD_MAC the
+ * plaintext is withheld (out is zero-filled), as the reference returns no
+ * plaintext with its Err (chacha20_poly1305.rs:89-93); the decryption itself
+ * always runs (:80-82).  Returns SG_OK, SG_E_BAD_MAC, SG_E_SHORT or < 0. */
+int sg_open(sg_ctx* ctx, const uint8_t* nonce, size_t nonce_len,
+            const uint8_t* in, size_t in_len, const uint8_t* ad, size_t adlen, uint8_t* out);
+
+/* ---- batch interface (record-layer batching point, tls.rs:140) --------- */
+#define SG_BATCH_TLS  0x1u  /* nonce = be64(seq_i); ad = be64(seq_i) || content_type ||
+                               ver_major || ver_minor || be16(n_i)  (tls.rs:103-112,
+                               250-265); `nonces`/`ads` are ignored               */
+
+typedef struct sg_batch {
+    uint32_t count;            /* number of records                                 */
+    uint32_t flags;            /* SG_BATCH_*                                        */
+
+    /* keys: key table [num_keys][32] in device memory; record i uses
+     * key_index[i] (device array) or key 0 when key_index is NULL.            */
+    const uint8_t*  keys;
+    uint32_t        num_keys;
+    const uint32_t* key_index;
+
+    /* TLS mode: seq_i = seq ? seq[i] : seq0 + i   (device array)            */
+    const uint64_t* seq;
+    uint64_t        seq0;
+    uint8_t         content_type;   /* 23 = application_data (tls.rs:26)     */
+    uint8_t         ver_major;      /* 3                                     */
+    uint8_t         ver_minor;      /* 3                                     */
+    uint8_t         _pad0;
+
+    /* explicit mode: nonce_i = nonces + 8*i; ad_i = ads + ad_stride*i, ad_len
+     * bytes (device memory)                                                   */
+    const uint8_t*  nonces;
+    const uint8_t*  ads;
+    uint32_t        ad_len;
+    uint32_t        ad_stride;
+
+    /* record layout (device memory).  Record i reads in + in_off_i and writes
+     * out + out_off_i, where off_i = off ? off[i] : stride * i.
+     *   seal: input = plaintext of len_i bytes, output = ct || tag (len_i + 16)
+     *   open: input = ct || tag of len_i bytes (len_i >= 16 else status
+     *         SG_E_SHORT), output = plaintext (len_i - 16)
+     * len_i = len ? len[i] : uniform_len.  max_len >= every len_i is required
+     * when len != NULL (it sizes the LDS staging of one record).              */
+    const uint8_t*  in;
+    const uint64_t* in_off;
+    uint64_t        in_stride;
+    uint8_t*        out;
+    const uint64_t* out_off;
+    uint64_t        out_stride;
+    const uint32_t* len;
+    uint32_t        uniform_len;
+    uint32_t        max_len;
+
+    /* open: per-record status (SG_OK / SG_E_BAD_MAC / SG_E_SHORT), device   */
+    uint8_t*        status;
+
+    /* HIP stream (hipStream_t) or NULL for the library's per-device stream.
+     * The call is asynchronous on that stream when `stream` is non-NULL.    */
+    void*           stream;
+
+    /* scratch of >= sg_workspace_size(count) bytes of device memory, or NULL
+     * to use a library-owned cache (grown on demand; not graph-capturable). */
+    void*           workspace;
+    size_t          workspace_size;
+} sg_batch;
+
+size_t sg_workspace_size(uint32_t count);
+
+/* Batch seal / open on device-resident records.  Records are independent
+ * (one workgroup each).  Returns SG_OK or < 0 for argument/HIP errors;
+ * per-record MAC results of open land in b->status. */
+int sg_seal_batch(const sg_batch* b);
+int sg_open_batch(const sg_batch* b);
+
+/* ---- synthetic workload helpers (bench / tests) ------------------------ */
+/* Fills records on the device: byte i of record j =
+ * byte (i mod 8) of splitmix64(seed ^ ((j0 + j) << 32) ^ (i / 8)).
+ * Records are len bytes each at buf + stride * j.                         */
+int sg_fill_records(uint8_t* buf, uint64_t stride, uint32_t len, uint32_t count,
+                    uint64_t seed, uint64_t j0, void* stream);
+/* Byte-compares a[j] and b[j] (len bytes at stride_a / stride_b); adds the
+ * number of mismatching records to *mismatches (device uint64).            */
+int sg_compare_records(const uint8_t* a, uint64_t stride_a, const uint8_t* b,
+                       uint64_t stride_b, uint32_t len, uint32_t count,
+                       unsigned long long* mismatches, void* stream);
+
+/* ---- diagnostics -------------------------------------------------------- */
+const char* sg_last_error(void);       /* thread-local message of the last failure */
+const char* sg_build_info(void);       /* arch + kernel configuration string       */
+/* Kernel timing with HIP events recorded on the launch stream.  While timing
+ * is enabled every batch call brackets its keying kernel and its seal/open
+ * kernel with events; sg_timing_read synchronises on them and returns the
+ * average duration (ms) per launch of each kind and the launch counts.
+ * sg_set_timing(1) resets the accumulators; sg_set_timing(0) stops them. */
+int sg_set_timing(int enable);
+int sg_timing_read(double* seal_ms, double* open_ms, double* keying_ms,
+                   uint32_t* n_seal, uint32_t* n_open, uint32_t* n_keying);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SURUGA_GPU_H */

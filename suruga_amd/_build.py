@@ -1,0 +1,81 @@
+"""Build recipes for the in-tree native artefacts.
+
+* ``suruga_amd/libsuruga_gpu.so`` -- the product: gfx950 HIP kernels + C ABI
+  (``include/suruga_gpu.h``), compiled with ``hipcc --offload-arch=gfx950``.
+* ``oracle/liboracle.so`` -- the CPU parity checker (test infrastructure only),
+  compiled with ``gcc`` from ``oracle/suruga_oracle.c``.
+
+Both are built in-tree so that they travel to the GPU box with the repo
+snapshot.  The reference (Rust, klutzy/suruga) cannot be compiled here: there
+is no rustc/cargo in the image, so there is no
+``oracle/_ref`` build.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+PKG = ROOT / "suruga_amd"
+CSRC = PKG / "csrc"
+LIB = PKG / "libsuruga_gpu.so"
+ORACLE_DIR = ROOT / "oracle"
+ORACLE_LIB = ORACLE_DIR / "liboracle.so"
+
+HIP_SOURCES = [CSRC / "sg_kernels.hip", CSRC / "sg_capi.cpp"]
+HIP_DEPS = HIP_SOURCES + [CSRC / "sg_internal.h", ROOT / "include" / "suruga_gpu.h"]
+ORACLE_SOURCES = [ORACLE_DIR / "suruga_oracle.c"]
+ORACLE_DEPS = ORACLE_SOURCES + [ORACLE_DIR / "suruga_oracle.h"]
+
+
+def _stale(target: Path, deps) -> bool:
+    if not target.exists():
+        return True
+    t = target.stat().st_mtime
+    return any(d.stat().st_mtime > t for d in deps)
+
+
+def _run(cmd) -> None:
+    proc = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True)
+    if proc.returncode != 0:
+        raise RuntimeError(f"build failed: {' '.join(map(str, cmd))}\n{proc.stdout}\n{proc.stderr}")
+
+
+def hipcc() -> str:
+    rocm = os.environ.get("ROCM_PATH", "/opt/rocm")
+    cand = Path(rocm) / "bin" / "hipcc"
+    return str(cand) if cand.exists() else "hipcc"
+
+
+def build_library(force: bool = False) -> Path:
+    """Compile the gfx950 HIP library (seconds)."""
+    if force or _stale(LIB, HIP_DEPS):
+        tmp = LIB.with_suffix(".so.tmp")
+        _run([hipcc(), "--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17",
+              "-Wall", "-Wno-unused-result", "-o", str(tmp), *map(str, HIP_SOURCES)])
+        os.replace(tmp, LIB)
+    return LIB
+
+
+def build_oracle(force: bool = False) -> Path:
+    """Compile the CPU restatement used as the parity checker."""
+    if force or _stale(ORACLE_LIB, ORACLE_DEPS):
+        tmp = ORACLE_LIB.with_suffix(".so.tmp")
+        _run(["gcc", "-O2", "-std=c11", "-Wall", "-Wextra", "-fPIC", "-shared", "-pthread",
+              "-o", str(tmp), *map(str, ORACLE_SOURCES)])
+        os.replace(tmp, ORACLE_LIB)
+    return ORACLE_LIB
+
+
+def build_all(force: bool = False) -> None:
+    build_library(force)
+    build_oracle(force)
+
+
+if __name__ == "__main__":
+    import sys
+
+    build_all(force="--force" in sys.argv)
+    print(LIB)
+    print(ORACLE_LIB)

@@ -1,0 +1,142 @@
+"""ctypes binding of the C ABI in ``include/suruga_gpu.h``.
+
+The shared library is the only compute path: if it is missing or cannot be
+loaded this module raises -- there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import threading
+from pathlib import Path
+
+from ._build import LIB
+
+SG_OK = 0
+SG_E_BAD_MAC = 1
+SG_E_SHORT = 2
+SG_E_ARG = -1
+SG_E_HIP = -2
+SG_E_NODEV = -3
+
+SG_BATCH_TLS = 0x1
+SG_KEY_LEN = 32
+SG_NONCE_LEN = 8
+SG_MAC_LEN = 16
+SG_MAX_AD_LEN = 255
+SG_MAX_RECORD_LEN = 32768
+
+# Every symbol include/suruga_gpu.h declares (checked by tests/test_abi.py).
+EXPORTS = [
+    "sg_key_size", "sg_fixed_iv_len", "sg_mac_len", "sg_abi_version",
+    "sg_ctx_new", "sg_ctx_free", "sg_seal", "sg_open",
+    "sg_workspace_size", "sg_seal_batch", "sg_open_batch",
+    "sg_fill_records", "sg_compare_records",
+    "sg_last_error", "sg_build_info", "sg_set_timing", "sg_timing_read",
+]
+
+
+class SgBatch(C.Structure):
+    """Mirror of ``struct sg_batch``."""
+
+    _fields_ = [
+        ("count", C.c_uint32),
+        ("flags", C.c_uint32),
+        ("keys", C.c_void_p),
+        ("num_keys", C.c_uint32),
+        ("key_index", C.c_void_p),
+        ("seq", C.c_void_p),
+        ("seq0", C.c_uint64),
+        ("content_type", C.c_uint8),
+        ("ver_major", C.c_uint8),
+        ("ver_minor", C.c_uint8),
+        ("_pad0", C.c_uint8),
+        ("nonces", C.c_void_p),
+        ("ads", C.c_void_p),
+        ("ad_len", C.c_uint32),
+        ("ad_stride", C.c_uint32),
+        ("in_", C.c_void_p),
+        ("in_off", C.c_void_p),
+        ("in_stride", C.c_uint64),
+        ("out", C.c_void_p),
+        ("out_off", C.c_void_p),
+        ("out_stride", C.c_uint64),
+        ("len", C.c_void_p),
+        ("uniform_len", C.c_uint32),
+        ("max_len", C.c_uint32),
+        ("status", C.c_void_p),
+        ("stream", C.c_void_p),
+        ("workspace", C.c_void_p),
+        ("workspace_size", C.c_size_t),
+    ]
+
+
+class NativeError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"suruga_gpu error {code}: {msg}")
+        self.code = code
+
+
+_lib = None
+_lock = threading.Lock()
+
+
+def _declare(lib: C.CDLL) -> None:
+    u8p = C.POINTER(C.c_uint8)
+    lib.sg_key_size.restype = C.c_size_t
+    lib.sg_fixed_iv_len.restype = C.c_size_t
+    lib.sg_mac_len.restype = C.c_size_t
+    lib.sg_abi_version.restype = C.c_int
+    lib.sg_ctx_new.restype = C.c_void_p
+    lib.sg_ctx_new.argtypes = [C.c_char_p, C.c_int]
+    lib.sg_ctx_free.restype = None
+    lib.sg_ctx_free.argtypes = [C.c_void_p]
+    for f in (lib.sg_seal, lib.sg_open):
+        f.restype = C.c_int
+        f.argtypes = [C.c_void_p, C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t,
+                      C.c_char_p, C.c_size_t, u8p]
+    lib.sg_workspace_size.restype = C.c_size_t
+    lib.sg_workspace_size.argtypes = [C.c_uint32]
+    for f in (lib.sg_seal_batch, lib.sg_open_batch):
+        f.restype = C.c_int
+        f.argtypes = [C.POINTER(SgBatch)]
+    lib.sg_fill_records.restype = C.c_int
+    lib.sg_fill_records.argtypes = [C.c_void_p, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint64,
+                                    C.c_uint64, C.c_void_p]
+    lib.sg_compare_records.restype = C.c_int
+    lib.sg_compare_records.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_uint32,
+                                       C.c_uint32, C.c_void_p, C.c_void_p]
+    lib.sg_last_error.restype = C.c_char_p
+    lib.sg_build_info.restype = C.c_char_p
+    lib.sg_set_timing.restype = C.c_int
+    lib.sg_set_timing.argtypes = [C.c_int]
+    lib.sg_timing_read.restype = C.c_int
+    d = C.POINTER(C.c_double)
+    u = C.POINTER(C.c_uint32)
+    lib.sg_timing_read.argtypes = [d, d, d, u, u, u]
+
+
+def load(path: Path | None = None) -> C.CDLL:
+    """Load (once) and return the native library.  Raises if it is missing."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            p = Path(path) if path else LIB
+            if not p.exists():
+                raise ImportError(
+                    f"{p} is missing: build it with `python -m suruga_amd._build` "
+                    "(hipcc --offload-arch=gfx950); there is no CPU fallback")
+            lib = C.CDLL(str(p))
+            _declare(lib)
+            _lib = lib
+        return _lib
+
+
+def last_error() -> str:
+    return load().sg_last_error().decode(errors="replace")
+
+
+def check(code: int) -> int:
+    """Raise NativeError for negative (argument / runtime) codes."""
+    if code < 0:
+        raise NativeError(code, last_error())
+    return code

@@ -1,0 +1,395 @@
+// sg_capi.cpp -- the C ABI declared in include/suruga_gpu.h.
+//
+// Host-side glue only: argument checking (mirroring the reference's panics /
+// errors), per-device state (stream, keying workspace cache, timing events),
+// staging for the single-record Encryptor/Decryptor calls, and the launches
+// of the gfx950 kernels in sg_kernels.hip.  There is no CPU fallback: every
+// seal/open goes through the HIP kernels or fails with an error code.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/suruga_gpu.h"
+#include "sg_internal.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, const char* detail = nullptr) {
+    char buf[512];
+    std::snprintf(buf, sizeof buf, fmt, detail ? detail : "");
+    g_err = buf;
+    return code;
+}
+
+int hip_fail(hipError_t e, const char* where) {
+    char buf[512];
+    std::snprintf(buf, sizeof buf, "%s: %s", where, hipGetErrorString(e));
+    g_err = buf;
+    return SG_E_HIP;
+}
+
+#define SG_HIP(call)                                           \
+    do {                                                       \
+        hipError_t e_ = (call);                                \
+        if (e_ != hipSuccess) return hip_fail(e_, #call);      \
+    } while (0)
+
+struct DeviceState {
+    bool init = false;
+    bool ok = false;
+    hipStream_t stream = nullptr;
+    void* ws = nullptr;
+    size_t ws_bytes = 0;
+};
+
+std::mutex g_mu;
+std::vector<DeviceState> g_dev;
+
+// timing
+struct TimedLaunch {
+    hipEvent_t a, b;
+    int kind;  // 0 keying, 1 seal, 2 open
+};
+bool g_timing = false;
+std::vector<TimedLaunch> g_timed;
+std::vector<hipEvent_t> g_event_pool;
+
+hipEvent_t get_event() {
+    if (!g_event_pool.empty()) {
+        hipEvent_t e = g_event_pool.back();
+        g_event_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+
+// Checks the device is a gfx950 part and creates its stream.  Caller holds g_mu.
+int device_state(int dev, DeviceState** out) {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+        return fail(SG_E_NODEV, "no HIP device visible%s");
+    if (dev < 0 || dev >= ndev) return fail(SG_E_ARG, "device ordinal out of range%s");
+    if ((int)g_dev.size() < ndev) g_dev.resize(ndev);
+    DeviceState& d = g_dev[dev];
+    if (!d.init) {
+        d.init = true;
+        hipDeviceProp_t prop;
+        SG_HIP(hipGetDeviceProperties(&prop, dev));
+        if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+            d.ok = false;
+            return fail(SG_E_NODEV, "device is %s, this library is built for gfx950 only", prop.gcnArchName);
+        }
+        SG_HIP(hipSetDevice(dev));
+        SG_HIP(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+        d.ok = true;
+    }
+    if (!d.ok) return fail(SG_E_NODEV, "device not usable%s");
+    *out = &d;
+    return SG_OK;
+}
+
+int current_device_state(DeviceState** out) {
+    int dev = 0;
+    SG_HIP(hipGetDevice(&dev));
+    return device_state(dev, out);
+}
+
+// Workspace from the per-device cache.  Caller holds g_mu.  Growing it frees
+// the old buffer, so it synchronises the device first.
+int cached_workspace(DeviceState* d, size_t need, void** ws) {
+    if (d->ws_bytes < need) {
+        SG_HIP(hipDeviceSynchronize());
+        if (d->ws) SG_HIP(hipFree(d->ws));
+        d->ws = nullptr;
+        d->ws_bytes = 0;
+        size_t sz = need < (1u << 20) ? (1u << 20) : need;
+        SG_HIP(hipMalloc(&d->ws, sz));
+        d->ws_bytes = sz;
+    }
+    *ws = d->ws;
+    return SG_OK;
+}
+
+int validate(const sg_batch* b, bool open) {
+    if (!b) return fail(SG_E_ARG, "batch is NULL%s");
+    if (b->count == 0) return SG_OK;
+    if (!b->keys || !b->in || !b->out) return fail(SG_E_ARG, "keys/in/out must be non-NULL%s");
+    if (((uintptr_t)b->keys & 3u) != 0) return fail(SG_E_ARG, "key table must be 4-byte aligned%s");
+    if (b->num_keys == 0) return fail(SG_E_ARG, "num_keys must be >= 1%s");
+    if (open && !b->status) return fail(SG_E_ARG, "open requires a status array%s");
+    if (b->flags & ~SG_BATCH_TLS) return fail(SG_E_ARG, "unknown flags%s");
+    if (!(b->flags & SG_BATCH_TLS)) {
+        if (!b->nonces) return fail(SG_E_ARG, "explicit mode needs nonces%s");
+        if (b->ad_len > SG_MAX_AD_LEN) return fail(SG_E_ARG, "ad_len exceeds SG_MAX_AD_LEN%s");
+        if (b->ad_len && !b->ads) return fail(SG_E_ARG, "ad_len > 0 needs ads%s");
+    }
+    uint32_t maxl = b->len ? b->max_len : b->uniform_len;
+    if (b->len && b->max_len == 0) return fail(SG_E_ARG, "max_len is required with len[]%s");
+    uint32_t max_n = open ? (maxl >= 16 ? maxl - 16 : 0) : maxl;
+    if (max_n > SG_MAX_RECORD_LEN) return fail(SG_E_ARG, "record longer than SG_MAX_RECORD_LEN%s");
+    if ((b->flags & SG_BATCH_TLS) && max_n > 0xffffu)
+        return fail(SG_E_ARG, "TLS mode record length must fit be16%s");
+    return SG_OK;
+}
+
+int run_batch(const sg_batch* b, bool open) {
+    int rc = validate(b, open);
+    if (rc != SG_OK || b->count == 0) return rc;
+
+    std::lock_guard<std::mutex> lk(g_mu);
+    DeviceState* d = nullptr;
+    rc = current_device_state(&d);
+    if (rc != SG_OK) return rc;
+    hipStream_t s = b->stream ? (hipStream_t)b->stream : d->stream;
+
+    void* ws = b->workspace;
+    const size_t need = sg_workspace_size(b->count);
+    if (ws) {
+        if (b->workspace_size < need) return fail(SG_E_ARG, "workspace too small%s");
+    } else {
+        rc = cached_workspace(d, need, &ws);
+        if (rc != SG_OK) return rc;
+    }
+
+    sg::KParams p;
+    std::memset(&p, 0, sizeof p);
+    p.keys = b->keys;
+    p.key_index = b->key_index;
+    p.seq = b->seq;
+    p.seq0 = b->seq0;
+    p.nonces = b->nonces;
+    p.ads = b->ads;
+    p.in = b->in;
+    p.in_off = b->in_off;
+    p.in_stride = b->in_stride;
+    p.out = b->out;
+    p.out_off = b->out_off;
+    p.out_stride = b->out_stride;
+    p.len = b->len;
+    p.status = b->status;
+    p.ws = (uint32_t*)ws;
+    p.uniform_len = b->uniform_len;
+    p.count = b->count;
+    p.tls = (b->flags & SG_BATCH_TLS) ? 1u : 0u;
+    p.ad_len = p.tls ? 13u : b->ad_len;
+    p.ad_stride = b->ad_stride;
+    p.tls_hdr = (uint32_t)b->content_type | ((uint32_t)b->ver_major << 8) | ((uint32_t)b->ver_minor << 16);
+    p.lds_ct_off = sg::lds_ct_off(p.ad_len);
+    const uint32_t maxl = b->len ? b->max_len : b->uniform_len;
+    const uint32_t lds = sg::lds_bytes(p.lds_ct_off, maxl);
+
+    hipEvent_t e[4] = {nullptr, nullptr, nullptr, nullptr};
+    if (g_timing)
+        for (auto& x : e) x = get_event();
+    if (g_timing) SG_HIP(hipEventRecord(e[0], s));
+    SG_HIP(sg::launch_keying(p, s));
+    if (g_timing) {
+        SG_HIP(hipEventRecord(e[1], s));
+        SG_HIP(hipEventRecord(e[2], s));
+    }
+    SG_HIP(open ? sg::launch_open(p, lds, s) : sg::launch_seal(p, lds, s));
+    if (g_timing) {
+        SG_HIP(hipEventRecord(e[3], s));
+        g_timed.push_back({e[0], e[1], 0});
+        g_timed.push_back({e[2], e[3], open ? 2 : 1});
+    }
+    if (!b->stream) SG_HIP(hipStreamSynchronize(s));
+    return SG_OK;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// single-record contexts (Encryptor / Decryptor)
+// ---------------------------------------------------------------------------
+struct sg_ctx {
+    int device;
+    uint8_t* d_key;      // 32 B
+    uint8_t* d_nonce;    // 8 B
+    uint8_t* d_ad;       // SG_MAX_AD_LEN
+    uint8_t* d_in;       // SG_MAX_RECORD_LEN + 16
+    uint8_t* d_out;      // SG_MAX_RECORD_LEN + 16
+    uint8_t* d_status;   // 1
+    void* d_ws;
+    hipStream_t stream;
+    std::mutex mu;
+};
+
+extern "C" {
+
+size_t sg_key_size(void) { return SG_KEY_LEN; }
+size_t sg_fixed_iv_len(void) { return 0; }
+size_t sg_mac_len(void) { return SG_MAC_LEN; }
+int sg_abi_version(void) { return SG_ABI_VERSION; }
+const char* sg_last_error(void) { return g_err.c_str(); }
+const char* sg_build_info(void) { return sg::kernel_config(); }
+size_t sg_workspace_size(uint32_t count) { return (size_t)count * sg::kKeyRecWords * 4u; }
+
+sg_ctx* sg_ctx_new(const uint8_t key[32], int device) {
+    if (!key) {
+        fail(SG_E_ARG, "key is NULL%s");
+        return nullptr;
+    }
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        DeviceState* d = nullptr;
+        if (device_state(device, &d) != SG_OK) return nullptr;
+    }
+    if (hipSetDevice(device) != hipSuccess) {
+        fail(SG_E_HIP, "hipSetDevice failed%s");
+        return nullptr;
+    }
+    sg_ctx* c = new sg_ctx();
+    c->device = device;
+    const size_t cap = SG_MAX_RECORD_LEN + 64;
+    bool ok = hipMalloc((void**)&c->d_key, 64) == hipSuccess &&
+              hipMalloc((void**)&c->d_nonce, 64) == hipSuccess &&
+              hipMalloc((void**)&c->d_ad, 512) == hipSuccess &&
+              hipMalloc((void**)&c->d_in, cap) == hipSuccess &&
+              hipMalloc((void**)&c->d_out, cap) == hipSuccess &&
+              hipMalloc((void**)&c->d_status, 64) == hipSuccess &&
+              hipMalloc(&c->d_ws, sg_workspace_size(1)) == hipSuccess &&
+              hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
+              hipMemcpy(c->d_key, key, 32, hipMemcpyHostToDevice) == hipSuccess;
+    if (!ok) {
+        fail(SG_E_HIP, "context allocation failed%s");
+        sg_ctx_free(c);
+        return nullptr;
+    }
+    return c;
+}
+
+void sg_ctx_free(sg_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    (void)hipFree(c->d_key);
+    (void)hipFree(c->d_nonce);
+    (void)hipFree(c->d_ad);
+    (void)hipFree(c->d_in);
+    (void)hipFree(c->d_out);
+    (void)hipFree(c->d_status);
+    (void)hipFree(c->d_ws);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+static int single(sg_ctx* c, bool open, const uint8_t* nonce, size_t nonce_len, const uint8_t* in,
+                  size_t in_len, const uint8_t* ad, size_t adlen, uint8_t* out) {
+    if (!c) return fail(SG_E_ARG, "context is NULL%s");
+    if (nonce_len != SG_NONCE_LEN || !nonce) return fail(SG_E_ARG, "nonce must be 8 bytes%s");
+    if (adlen > SG_MAX_AD_LEN || (adlen && !ad)) return fail(SG_E_ARG, "bad additional data%s");
+    if ((in_len && !in) || !out) return fail(SG_E_ARG, "NULL buffer%s");
+    if (open && in_len < SG_MAC_LEN) return SG_E_SHORT;  // chacha20_poly1305.rs:68-70
+    const size_t n = open ? in_len - SG_MAC_LEN : in_len;
+    if (n > SG_MAX_RECORD_LEN) return fail(SG_E_ARG, "record longer than SG_MAX_RECORD_LEN%s");
+
+    std::lock_guard<std::mutex> lk(c->mu);
+    SG_HIP(hipSetDevice(c->device));
+    SG_HIP(hipMemcpyAsync(c->d_nonce, nonce, 8, hipMemcpyHostToDevice, c->stream));
+    if (adlen) SG_HIP(hipMemcpyAsync(c->d_ad, ad, adlen, hipMemcpyHostToDevice, c->stream));
+    if (in_len) SG_HIP(hipMemcpyAsync(c->d_in, in, in_len, hipMemcpyHostToDevice, c->stream));
+
+    sg_batch b;
+    std::memset(&b, 0, sizeof b);
+    b.count = 1;
+    b.keys = c->d_key;
+    b.num_keys = 1;
+    b.nonces = c->d_nonce;
+    b.ads = c->d_ad;
+    b.ad_len = (uint32_t)adlen;
+    b.ad_stride = (uint32_t)adlen;
+    b.in = c->d_in;
+    b.in_stride = in_len;
+    b.out = c->d_out;
+    b.out_stride = in_len + 16;
+    b.uniform_len = (uint32_t)in_len;
+    b.status = c->d_status;
+    b.stream = c->stream;
+    b.workspace = c->d_ws;
+    b.workspace_size = sg_workspace_size(1);
+    int rc = open ? sg_open_batch(&b) : sg_seal_batch(&b);
+    if (rc != SG_OK) return rc;
+    const size_t out_len = open ? n : n + SG_MAC_LEN;
+    uint8_t st = 0;
+    if (out_len) SG_HIP(hipMemcpyAsync(out, c->d_out, out_len, hipMemcpyDeviceToHost, c->stream));
+    if (open) SG_HIP(hipMemcpyAsync(&st, c->d_status, 1, hipMemcpyDeviceToHost, c->stream));
+    SG_HIP(hipStreamSynchronize(c->stream));
+    if (open && st != 0) {
+        if (n) std::memset(out, 0, n);  // the reference releases no plaintext with Err
+        return st == 2 ? SG_E_SHORT : SG_E_BAD_MAC;
+    }
+    return SG_OK;
+}
+
+int sg_seal(sg_ctx* c, const uint8_t* nonce, size_t nonce_len, const uint8_t* pt, size_t n,
+            const uint8_t* ad, size_t adlen, uint8_t* out) {
+    return single(c, false, nonce, nonce_len, pt, n, ad, adlen, out);
+}
+
+int sg_open(sg_ctx* c, const uint8_t* nonce, size_t nonce_len, const uint8_t* in, size_t in_len,
+            const uint8_t* ad, size_t adlen, uint8_t* out) {
+    return single(c, true, nonce, nonce_len, in, in_len, ad, adlen, out);
+}
+
+int sg_seal_batch(const sg_batch* b) { return run_batch(b, false); }
+int sg_open_batch(const sg_batch* b) { return run_batch(b, true); }
+
+int sg_fill_records(uint8_t* buf, uint64_t stride, uint32_t len, uint32_t count, uint64_t seed, uint64_t j0,
+                    void* stream) {
+    if (!buf && count) return fail(SG_E_ARG, "buf is NULL%s");
+    SG_HIP(sg::launch_fill(buf, stride, len, count, seed, j0, (hipStream_t)stream));
+    if (!stream) SG_HIP(hipStreamSynchronize(nullptr));
+    return SG_OK;
+}
+
+int sg_compare_records(const uint8_t* a, uint64_t sa, const uint8_t* b, uint64_t sb, uint32_t len,
+                       uint32_t count, unsigned long long* mism, void* stream) {
+    if ((!a || !b || !mism) && count) return fail(SG_E_ARG, "NULL pointer%s");
+    SG_HIP(sg::launch_compare(a, sa, b, sb, len, count, mism, (hipStream_t)stream));
+    if (!stream) SG_HIP(hipStreamSynchronize(nullptr));
+    return SG_OK;
+}
+
+int sg_set_timing(int enable) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    for (auto& t : g_timed) {
+        (void)hipEventSynchronize(t.b);
+        g_event_pool.push_back(t.a);
+        g_event_pool.push_back(t.b);
+    }
+    g_timed.clear();
+    g_timing = enable != 0;
+    return SG_OK;
+}
+
+int sg_timing_read(double* seal_ms, double* open_ms, double* keying_ms, uint32_t* n_seal, uint32_t* n_open,
+                   uint32_t* n_keying) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    double sum[3] = {0, 0, 0};
+    uint32_t cnt[3] = {0, 0, 0};
+    for (auto& t : g_timed) {
+        SG_HIP(hipEventSynchronize(t.b));
+        float ms = 0.f;
+        SG_HIP(hipEventElapsedTime(&ms, t.a, t.b));
+        sum[t.kind] += ms;
+        cnt[t.kind] += 1;
+    }
+    if (keying_ms) *keying_ms = cnt[0] ? sum[0] / cnt[0] : 0.0;
+    if (seal_ms) *seal_ms = cnt[1] ? sum[1] / cnt[1] : 0.0;
+    if (open_ms) *open_ms = cnt[2] ? sum[2] / cnt[2] : 0.0;
+    if (n_keying) *n_keying = cnt[0];
+    if (n_seal) *n_seal = cnt[1];
+    if (n_open) *n_open = cnt[2];
+    return SG_OK;
+}
+
+}  // extern "C"

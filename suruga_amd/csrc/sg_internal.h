@@ -1,0 +1,59 @@
+// sg_internal.h -- shared between the HIP kernels (sg_kernels.hip) and the
+// C-ABI host layer (sg_capi.cpp).  Not part of the public ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace sg {
+
+constexpr uint32_t kThreads = 256;        // one record per 256-thread workgroup
+constexpr uint32_t kKeyRecWords = 40;     // per-record keying output (u32 words)
+// keying record layout: pw[7][5] = r^(2^k) in radix 2^26 (k = 0..6: r .. r^64),
+// then s[4] (second half of keystream block 0), then one pad word.
+constexpr uint32_t kPowOff = 0;
+constexpr uint32_t kSOff = 35;
+
+// Kernel parameters (passed by value as kernarg).
+struct KParams {
+    const uint8_t* keys;
+    const uint32_t* key_index;
+    const uint64_t* seq;
+    uint64_t seq0;
+    const uint8_t* nonces;
+    const uint8_t* ads;
+    const uint8_t* in;
+    const uint64_t* in_off;
+    uint64_t in_stride;
+    uint8_t* out;
+    const uint64_t* out_off;
+    uint64_t out_stride;
+    const uint32_t* len;
+    uint8_t* status;
+    uint32_t* ws;            // count * kKeyRecWords
+    uint32_t uniform_len;
+    uint32_t count;
+    uint32_t ad_len;         // explicit mode
+    uint32_t ad_stride;
+    uint32_t tls;            // 1 = SG_BATCH_TLS
+    uint32_t tls_hdr;        // content_type | major << 8 | minor << 16
+    uint32_t lds_ct_off;     // LDS offset of ciphertext byte 0 (16-aligned)
+    uint32_t pad;
+};
+
+// LDS bytes one workgroup needs for records of at most max_n payload bytes.
+inline uint32_t lds_ct_off(uint32_t adlen) { return (adlen + 8 + 15) & ~15u; }
+inline uint32_t lds_bytes(uint32_t ct_off, uint32_t max_n) {
+    return ct_off + ((max_n + 63) & ~63u) + 64;
+}
+
+hipError_t launch_keying(const KParams& p, hipStream_t s);
+hipError_t launch_seal(const KParams& p, uint32_t lds, hipStream_t s);
+hipError_t launch_open(const KParams& p, uint32_t lds, hipStream_t s);
+hipError_t launch_fill(uint8_t* buf, uint64_t stride, uint32_t len, uint32_t count, uint64_t seed,
+                       uint64_t j0, hipStream_t s);
+hipError_t launch_compare(const uint8_t* a, uint64_t sa, const uint8_t* b, uint64_t sb, uint32_t len,
+                          uint32_t count, unsigned long long* mism, hipStream_t s);
+const char* kernel_config();
+
+}  // namespace sg

@@ -1,0 +1,274 @@
+"""GPU parity: the gfx950 kernels (through the C ABI) against the oracle and
+the committed fixtures.  Bit-exact on every byte of ciphertext, tag and
+plaintext; open status equal to the reference's Ok/Err(BadRecordMac).
+
+Configs (BASELINE.json): C0 = 1K x 1 KiB (full check), C1 = 1M x 16 KiB
+(checked here on a 4096-record subset byte for byte, and at 65536 records by
+round trip + XOR-fold of every tag against the multi-threaded oracle),
+C2 = Zipf sizes with 256 keys (checked on a sample), plus ragged lengths,
+misaligned offsets, explicit nonces/AD of every length class, tampering.
+"""
+from __future__ import annotations
+
+import hashlib
+import os
+import struct
+
+import numpy as np
+import pytest
+
+from conftest import vector_pt
+
+pytestmark = pytest.mark.gpu
+
+SEED = 0x53555255
+KEY = bytes(range(32))
+
+
+def torch_mod():
+    import torch
+
+    return torch
+
+
+def dev_bytes(b: bytes):
+    torch = torch_mod()
+    t = torch.frombuffer(bytearray(b) if b else bytearray(1), dtype=torch.uint8)
+    return t[:len(b)].to("cuda") if b else torch.zeros(1, dtype=torch.uint8, device="cuda")
+
+
+def host(t) -> bytes:
+    return bytes(t.cpu().numpy().tobytes())
+
+
+# ---------------------------------------------------------------------------
+# single-record Encryptor / Decryptor (the trait-object path, tls.rs:114, 268)
+# ---------------------------------------------------------------------------
+def test_single_record_vectors(gpu, oracle, aead_vectors):
+    from suruga_amd import ChaCha20Poly1305, TlsError, TlsErrorKind
+
+    aead = ChaCha20Poly1305()
+    for v in aead_vectors["vectors"]:
+        key, nonce, ad = bytes.fromhex(v["key"]), bytes.fromhex(v["nonce"]), bytes.fromhex(v["ad"])
+        pt = vector_pt(v, oracle)
+        enc, dec = aead.new_encryptor(key), aead.new_decryptor(key)
+        out = enc.encrypt(nonce, pt, ad)
+        if "ct_tag" in v:
+            assert out.hex() == v["ct_tag"], v["name"]
+        assert out[-16:].hex() == v["tag"], v["name"]
+        assert hashlib.sha256(out[:-16]).hexdigest() == v["ct_sha256"], v["name"]
+        assert dec.decrypt(nonce, out, ad) == pt, v["name"]
+        assert dec.mac_len() == 16
+        bad = bytearray(out)
+        bad[-1] ^= 0x80
+        with pytest.raises(TlsError) as e:
+            dec.decrypt(nonce, bytes(bad), ad)
+        assert e.value.kind is TlsErrorKind.BadRecordMac and e.value.desc == "wrong mac"
+
+
+def test_single_record_tamper_and_short(gpu, oracle, aead_vectors):
+    from suruga_amd import ChaCha20Poly1305, TlsError, TlsErrorKind
+
+    by_name = {v["name"]: v for v in aead_vectors["vectors"]}
+    aead = ChaCha20Poly1305()
+    for t in aead_vectors["tamper"]:
+        v = by_name[t["vector"]]
+        key, nonce, ad = bytes.fromhex(v["key"]), bytes.fromhex(v["nonce"]), bytes.fromhex(v["ad"])
+        data = bytearray(aead.new_encryptor(key).encrypt(nonce, vector_pt(v, oracle), ad))
+        data[t["flip"]] ^= 0x01
+        with pytest.raises(TlsError) as e:
+            aead.new_decryptor(key).decrypt(nonce, bytes(data), ad)
+        assert e.value.kind is TlsErrorKind.BadRecordMac
+    dec = aead.new_decryptor(KEY)
+    for s in aead_vectors["short"]:
+        with pytest.raises(TlsError) as e:
+            dec.decrypt(bytes(8), bytes(s["len"]), b"")
+        assert e.value.kind is TlsErrorKind.BadRecordMac and e.value.desc == "message too short"
+    # exactly 16 bytes = empty plaintext + tag: valid when produced by seal
+    out = aead.new_encryptor(KEY).encrypt(bytes(8), b"", b"")
+    assert len(out) == 16 and dec.decrypt(bytes(8), out, b"") == b""
+
+
+def test_single_record_random_lengths(gpu, oracle):
+    from suruga_amd import ChaCha20Poly1305
+
+    rng = np.random.default_rng(7)
+    aead = ChaCha20Poly1305()
+    for _ in range(60):
+        n = int(rng.integers(0, 18433))
+        adlen = int(rng.integers(0, 256))
+        key = rng.bytes(32)
+        nonce, ad, pt = rng.bytes(8), rng.bytes(adlen), rng.bytes(n)
+        out = aead.new_encryptor(key).encrypt(nonce, pt, ad)
+        assert out == oracle.seal(key, nonce, pt, ad), (n, adlen)
+        assert aead.new_decryptor(key).decrypt(nonce, out, ad) == pt
+
+
+# ---------------------------------------------------------------------------
+# batch, TLS mode
+# ---------------------------------------------------------------------------
+def tls_batch(count, n, *, seq0=0, key=KEY, j0=0):
+    """Device plaintext (fill rule), sealed + opened through the batch ABI."""
+    torch = torch_mod()
+    from suruga_amd import batch as B
+
+    keys = dev_bytes(key).view(1, 32)
+    pt = torch.empty(count * n if n else 1, dtype=torch.uint8, device="cuda")
+    if n:
+        B.fill_records(pt, n, n, count, SEED, j0)
+    ct = torch.empty(count * (n + 16), dtype=torch.uint8, device="cuda")
+    B.seal(B.Batch(count=count, keys=keys, inp=pt, out=ct, uniform_len=n, in_stride=n,
+                   out_stride=n + 16, seq0=seq0))
+    back = torch.empty(count * n if n else 1, dtype=torch.uint8, device="cuda")
+    st = torch.full((count,), 0xFF, dtype=torch.uint8, device="cuda")
+    B.open_(B.Batch(count=count, keys=keys, inp=ct, out=back, uniform_len=n + 16, in_stride=n + 16,
+                    out_stride=n, seq0=seq0, status=st))
+    torch.cuda.synchronize()
+    return pt, ct, back, st
+
+
+def test_c0_1k_x_1kib_bit_exact(gpu, oracle):
+    count, n = 1024, 1024
+    pt, ct, back, st = tls_batch(count, n)
+    pt_h = host(pt)
+    assert pt_h == b"".join(oracle.fill_record(SEED, j, n) for j in range(count))
+    assert host(ct) == oracle.seal_batch_tls(KEY, 0, pt_h, n, count, threads=8)
+    assert host(back) == pt_h
+    assert host(st) == bytes(count)
+
+
+def test_c1_subset_4096_x_16kib_bit_exact(gpu, oracle):
+    count, n = 4096, 16384
+    pt, ct, back, st = tls_batch(count, n, seq0=1000)
+    pt_h = host(pt)
+    assert host(ct) == oracle.seal_batch_tls(KEY, 1000, pt_h, n, count, threads=16)
+    assert host(back) == pt_h and host(st) == bytes(count)
+
+
+@pytest.mark.parametrize("n", [0, 1, 15, 16, 17, 63, 64, 65, 100, 255, 256, 1000, 4095, 16383, 16384, 18432])
+def test_batch_lengths(gpu, oracle, n):
+    count = 33
+    pt, ct, back, st = tls_batch(count, n, seq0=0xFFFFFFF0)
+    pt_h = host(pt)[:count * n]
+    assert host(ct) == oracle.seal_batch_tls(KEY, 0xFFFFFFF0, pt_h, n, count, threads=4)
+    assert host(back)[:count * n] == pt_h and host(st) == bytes(count)
+
+
+def test_batch_seq_edges(gpu, oracle):
+    torch = torch_mod()
+    from suruga_amd import batch as B
+
+    seqs = [0, 1, 0xFFFFFFFF, 0x100000000, 0xFFFFFFFFFFFFFFFF, 0x0123456789ABCDEF]
+    n, count = 300, len(seqs)
+    pt_h = b"".join(oracle.fill_record(SEED, j, n) for j in range(count))
+    keys = dev_bytes(KEY).view(1, 32)
+    seq_t = torch.tensor(np.array(seqs, dtype=np.uint64).view(np.int64), device="cuda")
+    pt = dev_bytes(pt_h)
+    ct = torch.empty(count * (n + 16), dtype=torch.uint8, device="cuda")
+    B.seal(B.Batch(count=count, keys=keys, inp=pt, out=ct, uniform_len=n, in_stride=n, out_stride=n + 16,
+                   seq=seq_t))
+    torch.cuda.synchronize()
+    got = host(ct)
+    for j, s in enumerate(seqs):
+        exp = oracle.seal(KEY, struct.pack(">Q", s), pt_h[j * n:(j + 1) * n], oracle.tls_ad(s, n))
+        assert got[j * (n + 16):(j + 1) * (n + 16)] == exp, hex(s)
+
+
+def test_batch_ragged_offsets_keys_and_tamper(gpu, oracle):
+    """C2-shaped: ragged lengths (incl. 0 and non-multiples of 16), 256-entry key
+    table, per-record key_index/seq, packed unaligned offsets; then open with one
+    tampered record and one truncated record."""
+    torch = torch_mod()
+    from suruga_amd import batch as B
+
+    rng = np.random.default_rng(11)
+    count = 700
+    lens = rng.integers(0, 4097, size=count).astype(np.uint32)
+    lens[:8] = [0, 1, 15, 16, 17, 63, 64, 65]
+    keys_h = rng.bytes(256 * 32)
+    kidx = (np.arange(count) % 256).astype(np.uint32)
+    seqs = (np.arange(count) // 256).astype(np.uint64)
+    gap = rng.integers(0, 7, size=count)  # unaligned packing
+    in_off = np.zeros(count, dtype=np.uint64)
+    out_off = np.zeros(count, dtype=np.uint64)
+    pos_i = pos_o = 0
+    for i in range(count):
+        pos_i += int(gap[i]); in_off[i] = pos_i; pos_i += int(lens[i])
+        pos_o += int(gap[i]); out_off[i] = pos_o; pos_o += int(lens[i]) + 16
+    pt_h = rng.bytes(pos_i + 16)
+    dev = lambda a: torch.from_numpy(a.view(np.int64) if a.dtype == np.uint64 else a.view(np.int32)).to("cuda")
+    keys = dev_bytes(keys_h).view(256, 32)
+    pt = dev_bytes(pt_h)
+    ct = torch.zeros(pos_o + 16, dtype=torch.uint8, device="cuda")
+    common = dict(count=count, keys=keys, key_index=dev(kidx), seq=dev(seqs), max_len=int(lens.max()) + 16)
+    B.seal(B.Batch(inp=pt, out=ct, lens=dev(lens), in_off=dev(in_off), out_off=dev(out_off), **common))
+    torch.cuda.synchronize()
+    ct_h = bytearray(host(ct))
+    for i in range(count):
+        k = keys_h[32 * kidx[i]:32 * kidx[i] + 32]
+        s, n = int(seqs[i]), int(lens[i])
+        exp = oracle.seal(k, struct.pack(">Q", s), pt_h[in_off[i]:in_off[i] + n], oracle.tls_ad(s, n))
+        assert bytes(ct_h[out_off[i]:out_off[i] + n + 16]) == exp, i
+    # open: tamper record 5, truncate record 9 to 10 bytes
+    ct_h[int(out_off[5])] ^= 1
+    olens = (lens + 16).astype(np.uint32)
+    olens[9] = 10
+    back = torch.zeros(pos_i + 16, dtype=torch.uint8, device="cuda")
+    st = torch.full((count,), 0xFF, dtype=torch.uint8, device="cuda")
+    B.open_(B.Batch(inp=dev_bytes(bytes(ct_h)), out=back, lens=dev(olens), in_off=dev(out_off),
+                    out_off=dev(in_off), status=st, **common))
+    torch.cuda.synchronize()
+    st_h = host(st)
+    exp_st = bytearray(count)
+    exp_st[5], exp_st[9] = 1, 2
+    assert st_h == bytes(exp_st)
+    back_h = host(back)
+    for i in range(count):
+        if i in (5, 9):
+            continue
+        assert back_h[in_off[i]:in_off[i] + lens[i]] == pt_h[in_off[i]:in_off[i] + lens[i]], i
+
+
+def test_batch_explicit_mode(gpu, oracle):
+    torch = torch_mod()
+    from suruga_amd import batch as B
+
+    rng = np.random.default_rng(3)
+    for adlen in (0, 5, 13, 32, 255):
+        count, n = 40, 777
+        nonces_h, ads_h, pt_h = rng.bytes(8 * count), rng.bytes(max(adlen, 1) * count), rng.bytes(n * count)
+        keys = dev_bytes(KEY).view(1, 32)
+        ct = torch.empty(count * (n + 16), dtype=torch.uint8, device="cuda")
+        B.seal(B.Batch(count=count, keys=keys, inp=dev_bytes(pt_h), out=ct, uniform_len=n, in_stride=n,
+                       out_stride=n + 16, tls=False, nonces=dev_bytes(nonces_h), ads=dev_bytes(ads_h),
+                       ad_len=adlen, ad_stride=max(adlen, 1)))
+        torch.cuda.synchronize()
+        got = host(ct)
+        for j in range(count):
+            ad = ads_h[j * max(adlen, 1):j * max(adlen, 1) + adlen]
+            exp = oracle.seal(KEY, nonces_h[8 * j:8 * j + 8], pt_h[j * n:(j + 1) * n], ad)
+            assert got[j * (n + 16):(j + 1) * (n + 16)] == exp, (adlen, j)
+
+
+def test_c1_scale_roundtrip_and_tag_fold(gpu, oracle):
+    """65536 x 16 KiB (1 GiB): every record round-trips on device, and the
+    XOR-fold of all 65536 tags equals the multi-threaded oracle's."""
+    torch = torch_mod()
+    from suruga_amd import batch as B
+
+    count, n = 65536, 16384
+    pt, ct, back, st = tls_batch(count, n, seq0=7)
+    mism = torch.zeros(1, dtype=torch.int64, device="cuda")
+    B.compare_records(pt, n, back, n, n, count, mism)
+    torch.cuda.synchronize()
+    assert int(mism.item()) == 0 and int(st.sum().item()) == 0
+    tags = ct.view(count, n + 16)[:, n:].cpu().numpy()
+    fold = np.bitwise_xor.reduce(tags, axis=0).tobytes()
+    ct_ref = oracle.seal_batch_tls(KEY, 7, host(pt), n, count, threads=min(16, os.cpu_count() or 1))
+    ref_tags = np.frombuffer(ct_ref, dtype=np.uint8).reshape(count, n + 16)[:, n:]
+    assert fold == np.bitwise_xor.reduce(ref_tags, axis=0).tobytes()
+    # and a strided sample of whole records byte for byte
+    ct_h = ct.view(count, n + 16)
+    ref = np.frombuffer(ct_ref, dtype=np.uint8).reshape(count, n + 16)
+    for i in list(range(0, count, 4099)) + [count // 2, count - 1]:
+        assert np.array_equal(ct_h[i].cpu().numpy(), ref[i]), i

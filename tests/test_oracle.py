@@ -1,0 +1,165 @@
+"""CPU tests: the oracle (C restatement of suruga's algorithm) against the
+reference's own known-answer tests and the generated AEAD fixtures.
+
+Mirrors the reference's unit tests:
+  chacha20.rs:162-228          check_keystream / test_chacha20
+  poly1305.rs:354-404          test_add / test_normalize / test_mult (Int1305 algebra)
+  poly1305.rs:406-458          test_poly1305_examples
+  chacha20_poly1305.rs         (no reference test) -> aead_vectors.json
+"""
+from __future__ import annotations
+
+import hashlib
+import struct
+
+import pytest
+
+from conftest import vector_pt
+
+P = (1 << 130) - 5
+
+
+def value(limbs):
+    return sum(v << (26 * i) for i, v in enumerate(limbs))
+
+
+# ---- chacha20.rs:162-228 ----------------------------------------------------
+def test_chacha20_keystream_kats(oracle, kats):
+    assert len(kats["chacha20"]) == 5
+    for v in kats["chacha20"]:
+        ks = bytes.fromhex(v["keystream"])
+        assert oracle.keystream(bytes.fromhex(v["key"]), bytes.fromhex(v["nonce"]), len(ks)) == ks, v["source"]
+
+
+def test_chacha20_rejects_bad_lengths(oracle):
+    # ChaCha20::new asserts key.len() == 32 and nonce.len() == 8 (chacha20.rs:26-27)
+    with pytest.raises(ValueError):
+        oracle.keystream(bytes(31), bytes(8), 1)
+    with pytest.raises(ValueError):
+        oracle.keystream(bytes(32), bytes(12), 1)
+
+
+def test_chacha20_stream_continues_across_calls(oracle, kats):
+    # encrypt() never resets the counter; the 256-byte KAT spans 4 blocks
+    v = kats["chacha20"][4]
+    ks = bytes.fromhex(v["keystream"])
+    assert len(ks) == 256
+    assert oracle.keystream(bytes.fromhex(v["key"]), bytes.fromhex(v["nonce"]), 100) == ks[:100]
+
+
+# ---- poly1305.rs:321-404 (Int1305 algebra) ----------------------------------
+def test_int1305_add_associative(oracle, kats):
+    coeffs = kats["int1305_coeffs"]
+    for a in coeffs:
+        for b in coeffs:
+            for c in coeffs:
+                abc = oracle.add(oracle.add(a, b), c)
+                bca = oracle.add(oracle.add(b, c), a)
+                acb = oracle.add(oracle.add(a, c), b)
+                assert oracle.normalize(abc) == oracle.normalize(bca) == oracle.normalize(acb)
+
+
+def test_int1305_normalize(oracle, kats):
+    p = [0x3fffffb, 0x3ffffff, 0x3ffffff, 0x3ffffff, 0x3ffffff]
+    assert oracle.normalize(p) == [0] * 5
+    large, small = [0, 10, 5, 10, 1 << 26], [5, 10, 5, 10, 0]
+    assert oracle.normalize(large) == small
+    assert oracle.normalize(small) == small
+    for a in kats["int1305_coeffs"]:
+        assert oracle.normalize(oracle.normalize(a)) == oracle.normalize(a)
+        assert value(oracle.normalize(a)) == value(a) % P
+
+
+def test_int1305_mult_associative_and_exact(oracle, kats):
+    coeffs = kats["int1305_coeffs"]
+    for a in coeffs:
+        for b in coeffs:
+            ab = oracle.mult(a, b)
+            assert value(ab) % P == (value(a) * value(b)) % P
+            for c in coeffs:
+                abc = oracle.normalize(oracle.mult(ab, c))
+                bca = oracle.normalize(oracle.mult(oracle.mult(b, c), a))
+                acb = oracle.normalize(oracle.mult(oracle.mult(a, c), b))
+                assert abc == bca == acb
+
+
+# ---- poly1305.rs:406-458 ----------------------------------------------------
+def test_poly1305_examples(oracle, kats):
+    assert len(kats["poly1305"]) == 4
+    for v in kats["poly1305"]:
+        tag = oracle.poly1305(bytes.fromhex(v["msg"]), bytes.fromhex(v["r"]), bytes.fromhex(v["s"]))
+        assert tag.hex() == v["tag"]
+
+
+# ---- AEAD (chacha20_poly1305.rs) fixtures ------------------------------------
+def test_aead_vectors_seal(oracle, aead_vectors):
+    for v in aead_vectors["vectors"]:
+        key, nonce, ad = bytes.fromhex(v["key"]), bytes.fromhex(v["nonce"]), bytes.fromhex(v["ad"])
+        pt = vector_pt(v, oracle)
+        out = oracle.seal(key, nonce, pt, ad)
+        if "ct_tag" in v:
+            assert out.hex() == v["ct_tag"], v["name"]
+        assert out[-16:].hex() == v["tag"], v["name"]
+        assert hashlib.sha256(out[:-16]).hexdigest() == v["ct_sha256"], v["name"]
+
+
+def test_aead_vectors_open_roundtrip(oracle, aead_vectors):
+    for v in aead_vectors["vectors"]:
+        key, nonce, ad = bytes.fromhex(v["key"]), bytes.fromhex(v["nonce"]), bytes.fromhex(v["ad"])
+        pt = vector_pt(v, oracle)
+        rc, back = oracle.open(key, nonce, oracle.seal(key, nonce, pt, ad), ad)
+        assert rc == 0 and back == pt, v["name"]
+
+
+def test_tls_nonce_and_ad_rules(oracle, aead_vectors):
+    # tls.rs:103-112: nonce = be64(seq), ad = be64(seq) || 23 || 3 || 3 || be16(n)
+    for v in aead_vectors["vectors"]:
+        if "tls_seq" not in v:
+            continue
+        seq, n = v["tls_seq"], v["n"]
+        assert bytes.fromhex(v["nonce"]) == struct.pack(">Q", seq)
+        assert bytes.fromhex(v["ad"]) == oracle.tls_ad(seq, n)
+
+
+def test_open_tamper_is_bad_record_mac(oracle, aead_vectors):
+    by_name = {v["name"]: v for v in aead_vectors["vectors"]}
+    for t in aead_vectors["tamper"]:
+        v = by_name[t["vector"]]
+        key, nonce, ad = bytes.fromhex(v["key"]), bytes.fromhex(v["nonce"]), bytes.fromhex(v["ad"])
+        data = bytearray(oracle.seal(key, nonce, vector_pt(v, oracle), ad))
+        data[t["flip"]] ^= 0x01
+        rc, _ = oracle.open(key, nonce, bytes(data), ad)
+        assert rc == 1  # BadRecordMac "wrong mac" (chacha20_poly1305.rs:89-90)
+        # wrong AD or nonce must also fail
+        rc, _ = oracle.open(key, nonce, oracle.seal(key, nonce, b"x", ad), ad + b"!")
+        assert rc == 1
+
+
+def test_open_short_is_bad_record_mac(oracle, aead_vectors):
+    for s in aead_vectors["short"]:
+        rc, _ = oracle.open(bytes(32), bytes(8), bytes(s["len"]), b"")
+        assert rc == 2  # "message too short" (chacha20_poly1305.rs:68-70)
+
+
+def test_batch_driver_matches_single(oracle):
+    key = bytes(range(32))
+    n, count = 100, 37
+    pt = b"".join(oracle.fill_record(0x53555255, j, n) for j in range(count))
+    ct1 = oracle.seal_batch_tls(key, 5, pt, n, count, threads=1)
+    ct4 = oracle.seal_batch_tls(key, 5, pt, n, count, threads=4)
+    assert ct1 == ct4
+    for j in (0, 17, 36):
+        seq = 5 + j
+        single = oracle.seal(key, struct.pack(">Q", seq), pt[j * n:(j + 1) * n], oracle.tls_ad(seq, n))
+        assert ct1[j * (n + 16):(j + 1) * (n + 16)] == single
+    bad, back, st = oracle.open_batch_tls(key, 5, ct1, n, count, threads=3)
+    assert bad == 0 and back == pt and st == bytes(count)
+
+
+def test_fill_record_rule(oracle):
+    # byte i of record j = byte (i mod 8) of splitmix64(seed ^ (j << 32) ^ (i / 8))
+    seed, j = 0x53555255, 3
+    buf = oracle.fill_record(seed, j, 20)
+    for i in range(20):
+        w = oracle.L.so_splitmix64(seed ^ (j << 32) ^ (i // 8))
+        assert buf[i] == (w >> (8 * (i % 8))) & 0xFF
