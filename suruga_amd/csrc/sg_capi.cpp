@@ -190,7 +190,7 @@ int run_batch(const sg_batch* b, bool open) {
     if (g_timing)
         for (auto& x : e) x = get_event();
     if (g_timing) SG_HIP(hipEventRecord(e[0], s));
-    SG_HIP(sg::launch_keying(p, s));
+    SG_HIP(sg::launch_keying(p, open, s));
     if (g_timing) {
         SG_HIP(hipEventRecord(e[1], s));
         SG_HIP(hipEventRecord(e[2], s));

@@ -9,10 +9,12 @@ namespace sg {
 
 constexpr uint32_t kThreads = 256;        // one record per 256-thread workgroup
 constexpr uint32_t kKeyRecWords = 40;     // per-record keying output (u32 words)
-// keying record layout: pw[7][5] = r^(2^k) in radix 2^26 (k = 0..6: r .. r^64),
-// then s[4] (second half of keystream block 0), then one pad word.
-constexpr uint32_t kPowOff = 0;
-constexpr uint32_t kSOff = 35;
+// keying record layout (u32 words): r[4] clamped Poly1305 r (radix 2^32),
+// s[4] (second half of keystream block 0), R[6][5] = r^(k*2^l), l = 0..5, in
+// radix 2^26 (k = MAC blocks per lane, see mac_geom in sg_kernels.hip), 2 pad.
+constexpr uint32_t kR32Off = 0;
+constexpr uint32_t kSOff = 4;
+constexpr uint32_t kPowOff = 8;
 
 // Kernel parameters (passed by value as kernarg).
 struct KParams {
@@ -41,13 +43,15 @@ struct KParams {
     uint32_t pad;
 };
 
-// LDS bytes one workgroup needs for records of at most max_n payload bytes.
-inline uint32_t lds_ct_off(uint32_t adlen) { return (adlen + 8 + 15) & ~15u; }
+// LDS offset of ciphertext byte 0 (16-aligned, after the zero region and the
+// ad || le64(adlen) prefix), and the LDS bytes one workgroup needs for records
+// of at most max_n payload bytes.
+uint32_t lds_ct_off(uint32_t adlen);
 inline uint32_t lds_bytes(uint32_t ct_off, uint32_t max_n) {
     return ct_off + ((max_n + 63) & ~63u) + 64;
 }
 
-hipError_t launch_keying(const KParams& p, hipStream_t s);
+hipError_t launch_keying(const KParams& p, bool open, hipStream_t s);
 hipError_t launch_seal(const KParams& p, uint32_t lds, hipStream_t s);
 hipError_t launch_open(const KParams& p, uint32_t lds, hipStream_t s);
 hipError_t launch_fill(uint8_t* buf, uint64_t stride, uint32_t len, uint32_t count, uint64_t seed,

@@ -4,26 +4,28 @@
 // Work decomposition (one TLS record per 256-thread workgroup):
 //
 //   sg_keying_kernel   one lane per record: ChaCha20 block 0 -> Poly1305 key
-//                      (r clamped, s) and the powers r, r^2, r^4 .. r^64 the
-//                      MAC kernels multiply by.  (chacha20_poly1305.rs:50,75;
-//                      poly1305.rs:197-205)
+//                      (r clamped, s; chacha20_poly1305.rs:50,75,32-39,
+//                      poly1305.rs:197-203) and the six powers
+//                      r^(k*2^l), l = 0..5, that combine the MAC lanes.
 //   sg_aead_kernel<OPEN>
 //     phase 1, all 4 waves: lane t owns 64-byte data blocks t, t+256, ...;
 //       computes keystream block b+1 in registers (chacha20.rs:53-135),
 //       XORs the record bytes (chacha20.rs:143-153), writes the result to HBM
 //       and the ciphertext into LDS.
 //     phase 2, wave 0: Poly1305 over ad || le64(|ad|) || ct || le64(|ct|)
-//       (chacha20_poly1305.rs:19-42) read from LDS.  Lane t runs Horner over
-//       MAC blocks t, t+64, t+128, ... with multiplier r^64, then a 6-level
-//       shuffle tree with r^1..r^32 combines the 64 partial sums; lane 0
-//       multiplies by r, reduces mod 2^130-5 and adds s (poly1305.rs:230-312).
-//       Seal appends the tag (chacha20_poly1305.rs:55); open compares it in
-//       constant time (:84-93) after having decrypted unconditionally (:80-82).
+//       (chacha20_poly1305.rs:19-42), read from LDS.  The B MAC blocks are
+//       preceded by z zero "virtual" blocks (leading zeros do not change a
+//       Horner polynomial) so that B + z = 64k; lane t runs the reference's
+//       Horner step h = (h + c) * r (poly1305.rs:213-228) over its k
+//       contiguous blocks in radix 2^32 with the clamped r, and a 6-level
+//       shuffle tree with multipliers r^(k*2^l) (radix 2^26) sums
+//       h_t * r^(k*(63-t)).  Lane 0 reduces mod 2^130-5, adds s
+//       (poly1305.rs:230-312) and seals (chacha20_poly1305.rs:55) or
+//       compares in constant time (:84-93) after decrypting
+//       unconditionally (:80-82).
 //
-// All Poly1305 arithmetic is exact mod p = 2^130 - 5 in radix 2^26 with
-// 64-bit v_mad_u64_u32 accumulation; the result equals the reference's
-// sequential Horner (poly1305.rs:207-228) because both compute the same
-// polynomial in the field and reduce it to the canonical representative.
+// All Poly1305 arithmetic is exact mod p = 2^130 - 5, so the tag equals the
+// reference's sequential Horner result bit for bit.
 #include "sg_internal.h"
 
 #include <stdint.h>
@@ -32,10 +34,20 @@ namespace sg {
 namespace {
 
 constexpr uint32_t M26 = (1u << 26) - 1;
+constexpr uint32_t kZeroRegion = 2048;  // LDS bytes of zeros in front of the MAC stream
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ uint32_t rotl32(uint32_t x, int n) { return (x << n) | (x >> (32 - n)); }
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+
+__device__ __forceinline__ u32x4 ld16(const void* p) {
+    return *reinterpret_cast<const u32x4*>(__builtin_assume_aligned(p, 16));
+}
+__device__ __forceinline__ void st16(void* p, u32x4 v) {
+    *reinterpret_cast<u32x4*>(__builtin_assume_aligned(p, 16)) = v;
+}
 
 // chacha20.rs:63-81
 #define SG_QR(a, b, c, d)                   \
@@ -64,14 +76,14 @@ __device__ __forceinline__ void chacha_block(uint32_t ks[16], const uint32_t k[8
     ks[12] = x12 + ctr; ks[13] = x13; ks[14] = x14 + n14; ks[15] = x15 + n15;
 }
 
-// ---- Poly1305 field arithmetic, radix 2^26 ------------------------------
+// ---- Poly1305 field arithmetic, radix 2^26 (general multiplier) ----------
 // Invariant of a "reduced" element: limbs 0,2,3,4 < 2^26, limb 1 < 2^26 + 2^8.
 struct F26 {
     uint32_t v0, v1, v2, v3, v4;
 };
 
-// returns a * b + c (mod p, reduced), b fully reduced (< 2^26 per limb),
-// a reduced, c limbs < 2^27.
+// returns a * b + c (mod p, reduced); b fully reduced (< 2^26 per limb),
+// a limbs < 2^27, c limbs < 2^27.
 __device__ __forceinline__ F26 mul_add(const F26 a, const uint32_t b0, const uint32_t b1,
                                        const uint32_t b2, const uint32_t b3, const uint32_t b4,
                                        const F26 c) {
@@ -103,13 +115,9 @@ __device__ __forceinline__ F26 mul_add(const F26 a, const uint32_t b0, const uin
     return h;
 }
 
-__device__ __forceinline__ F26 mul_add(const F26 a, const uint32_t* b, const F26 c) {
-    return mul_add(a, b[0], b[1], b[2], b[3], b[4], c);
-}
-
 __device__ __forceinline__ F26 f26_zero() { return F26{0u, 0u, 0u, 0u, 0u}; }
 
-// Full carry: every limb < 2^26, value < 2^130 (not yet < p).
+// Full carry: every limb < 2^26 (value < 2^130, not yet < p).
 __device__ __forceinline__ F26 carry_full(F26 h) {
 #pragma unroll
     for (int pass = 0; pass < 2; ++pass) {
@@ -159,17 +167,76 @@ __device__ __forceinline__ void tag_words(F26 h, const uint32_t s[4], uint32_t t
     t[3] = (uint32_t)acc;
 }
 
-// 16 little-endian bytes (4 words) + the 2^(8*valid) pad bit -> radix-2^26
-// (poly1305.rs:130-162, :216-225).  valid in [1, 16].
-__device__ __forceinline__ F26 block_to_f26(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3,
-                                            uint32_t hibit) {
+// 128-bit little-endian value (4 words) + extra high bits -> radix 2^26
+__device__ __forceinline__ F26 words_to_f26(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3,
+                                            uint32_t hi) {
     F26 c;
     c.v0 = w0 & M26;
     c.v1 = __builtin_amdgcn_alignbit(w1, w0, 26) & M26;
     c.v2 = __builtin_amdgcn_alignbit(w2, w1, 20) & M26;
     c.v3 = __builtin_amdgcn_alignbit(w3, w2, 14) & M26;
-    c.v4 = (w3 >> 8) | hibit;
+    c.v4 = (w3 >> 8) | (hi << 24);
     return c;
+}
+
+// ---- Poly1305 Horner step with the clamped r, radix 2^32 ------------------
+// h = h0 + h1 2^32 + h2 2^64 + h3 2^96 + h4 2^128 (h4 small).  r0..r3 are the
+// clamped key words: r0 < 2^28, r1..r3 < 2^28 and divisible by 4, so
+// r_j 2^128 == (r_j / 4) * 5 (mod p) and s_j = r_j + (r_j >> 2) stays exact.
+struct H32 {
+    uint32_t h0, h1, h2, h3, h4;
+};
+
+__device__ __forceinline__ uint32_t addc(uint32_t a, uint32_t b, uint32_t cin, uint32_t* cout) {
+    return __builtin_addc(a, b, cin, cout);  // v_add_co / v_addc_co chain
+}
+
+// h = (h + m + pad * 2^128) * r  (partially reduced: h4 <= 4)
+__device__ __forceinline__ void horner_step(H32& h, uint32_t m0, uint32_t m1, uint32_t m2, uint32_t m3,
+                                            uint32_t pad, uint32_t r0, uint32_t r1, uint32_t r2,
+                                            uint32_t r3, uint32_t s1, uint32_t s2, uint32_t s3) {
+    // h += m (poly1305.rs:227 c.add(&h))
+    uint32_t c;
+    const uint32_t a0 = addc(h.h0, m0, 0u, &c);
+    const uint32_t a1 = addc(h.h1, m1, c, &c);
+    const uint32_t a2 = addc(h.h2, m2, c, &c);
+    const uint32_t a3 = addc(h.h3, m3, c, &c);
+    const uint32_t a4 = h.h4 + pad + c;
+    // * r (poly1305.rs:227 .mult(&r)): column sums < 2^63, then one carry ripple
+    const uint64_t d0 = (uint64_t)a0 * r0 + (uint64_t)a1 * s3 + (uint64_t)a2 * s2 + (uint64_t)a3 * s1;
+    const uint64_t d1 = (uint64_t)a0 * r1 + (uint64_t)a1 * r0 + (uint64_t)a2 * s3 + (uint64_t)a3 * s2 +
+                        (uint64_t)a4 * s1;
+    const uint64_t d2 = (uint64_t)a0 * r2 + (uint64_t)a1 * r1 + (uint64_t)a2 * r0 + (uint64_t)a3 * s3 +
+                        (uint64_t)a4 * s2;
+    const uint64_t d3 = (uint64_t)a0 * r3 + (uint64_t)a1 * r2 + (uint64_t)a2 * r1 + (uint64_t)a3 * r0 +
+                        (uint64_t)a4 * s3;
+    const uint32_t e1 = addc((uint32_t)d1, (uint32_t)(d0 >> 32), 0u, &c);
+    const uint32_t e2 = addc((uint32_t)d2, (uint32_t)(d1 >> 32), c, &c);
+    const uint32_t e3 = addc((uint32_t)d3, (uint32_t)(d2 >> 32), c, &c);
+    uint32_t e4 = a4 * r0 + (uint32_t)(d3 >> 32) + c;
+    // fold bits >= 2^130: (e4 >> 2) * 2^130 == (e4 >> 2) * 5
+    const uint32_t f = (e4 >> 2) * 5u;
+    e4 &= 3u;
+    h.h0 = addc((uint32_t)d0, f, 0u, &c);
+    h.h1 = addc(e1, 0u, c, &c);
+    h.h2 = addc(e2, 0u, c, &c);
+    h.h3 = addc(e3, 0u, c, &c);
+    h.h4 = e4 + c;
+}
+
+// MAC geometry: stream length L, blocks B, lane chunk k (odd: spreads the
+// lanes' LDS reads over banks), leading virtual zero blocks z = 64k - B.
+struct MacGeom {
+    uint32_t L, B, k, z;
+};
+__device__ __forceinline__ MacGeom mac_geom(uint32_t adlen, uint32_t n) {
+    MacGeom g;
+    g.L = adlen + 16u + n;
+    g.B = (g.L + 15u) >> 4;
+    g.k = (g.B + 63u) >> 6;
+    g.k |= 1u;
+    g.z = 64u * g.k - g.B;
+    return g;
 }
 
 // Per-record parameters shared by the keying and AEAD kernels.
@@ -207,30 +274,43 @@ __device__ __forceinline__ uint32_t record_len(const KParams& p, uint32_t rec) {
 // ---------------------------------------------------------------------------
 // Keying pre-pass: one lane per record.
 // ---------------------------------------------------------------------------
+template <bool OPEN>
 __global__ __launch_bounds__(256) void sg_keying_kernel(const KParams p) {
     const uint32_t rec = blockIdx.x * blockDim.x + threadIdx.x;
     if (rec >= p.count) return;
+    const uint32_t len = record_len(p, rec);
+    const uint32_t n = OPEN ? (len >= 16u ? len - 16u : 0u) : len;
     const RecKey rk = record_key(p, rec);
     uint32_t ks[16];
     chacha_block(ks, rk.k, 0u, rk.n14, rk.n15);  // block 0 -> poly key (chacha20_poly1305.rs:50)
     // r = clamp(pk[0..16]) (poly1305.rs:197-203), s = pk[16..32]
     const uint32_t r0 = ks[0] & 0x0fffffffu, r1 = ks[1] & 0x0ffffffcu;
     const uint32_t r2 = ks[2] & 0x0ffffffcu, r3 = ks[3] & 0x0ffffffcu;
-    F26 pw = block_to_f26(r0, r1, r2, r3, 0u);
     uint32_t* out = p.ws + (uint64_t)rec * kKeyRecWords;
-    for (int k = 0; k < 7; ++k) {
-        out[kPowOff + 5 * k + 0] = pw.v0;
-        out[kPowOff + 5 * k + 1] = pw.v1;
-        out[kPowOff + 5 * k + 2] = pw.v2;
-        out[kPowOff + 5 * k + 3] = pw.v3;
-        out[kPowOff + 5 * k + 4] = pw.v4;
-        if (k < 6) pw = carry_full(mul_add(pw, pw.v0, pw.v1, pw.v2, pw.v3, pw.v4, f26_zero()));
-    }
+    out[kR32Off + 0] = r0;
+    out[kR32Off + 1] = r1;
+    out[kR32Off + 2] = r2;
+    out[kR32Off + 3] = r3;
     out[kSOff + 0] = ks[4];
     out[kSOff + 1] = ks[5];
     out[kSOff + 2] = ks[6];
     out[kSOff + 3] = ks[7];
-    out[kSOff + 4] = 0u;
+    // R = r^k by square-and-multiply, then R^(2^l) for the lane-combining tree
+    const MacGeom g = mac_geom(p.tls ? 13u : p.ad_len, n);
+    const F26 r = words_to_f26(r0, r1, r2, r3, 0u);
+    F26 R = r;
+    for (int bit = 30 - __builtin_clz(g.k); bit >= 0; --bit) {
+        R = carry_full(mul_add(R, R.v0, R.v1, R.v2, R.v3, R.v4, f26_zero()));
+        if ((g.k >> bit) & 1u) R = carry_full(mul_add(R, r.v0, r.v1, r.v2, r.v3, r.v4, f26_zero()));
+    }
+    for (int l = 0; l < 6; ++l) {
+        out[kPowOff + 5 * l + 0] = R.v0;
+        out[kPowOff + 5 * l + 1] = R.v1;
+        out[kPowOff + 5 * l + 2] = R.v2;
+        out[kPowOff + 5 * l + 3] = R.v3;
+        out[kPowOff + 5 * l + 4] = R.v4;
+        if (l < 5) R = carry_full(mul_add(R, R.v0, R.v1, R.v2, R.v3, R.v4, f26_zero()));
+    }
 }
 
 // AD byte i of the TLS record-layer additional data (tls.rs:103-112, 250-265):
@@ -242,8 +322,11 @@ __device__ __forceinline__ uint8_t tls_ad_byte(uint64_t seq, uint32_t hdr, uint3
     return (uint8_t)n;
 }
 
+__device__ __forceinline__ uint32_t uniform(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+
 // ---------------------------------------------------------------------------
 // Fused seal / open: one record per workgroup.
+// LDS: [0, S) zeros | S: ad | le64(adlen) | A: ct (n) | le64(n) | zeros
 // ---------------------------------------------------------------------------
 template <bool OPEN>
 __global__ __launch_bounds__(256) void sg_aead_kernel(const KParams p) {
@@ -272,21 +355,28 @@ __global__ __launch_bounds__(256) void sg_aead_kernel(const KParams p) {
     for (uint32_t b = tid; b < nblocks; b += kThreads) {
         const uint32_t off = b << 6;
         if (vec_ok && off + 64u <= n) {
-            const uint4* src = reinterpret_cast<const uint4*>(in + off);
-            const uint4 d0 = src[0], d1 = src[1], d2 = src[2], d3 = src[3];
+            const u32x4 d0 = ld16(in + off), d1 = ld16(in + off + 16);
+            const u32x4 d2 = ld16(in + off + 32), d3 = ld16(in + off + 48);
             uint32_t ks[16];
             chacha_block(ks, rk.k, b + 1u, rk.n14, rk.n15);  // data uses blocks 1.. (chacha20_poly1305.rs:52)
-            const uint4 r0 = make_uint4(d0.x ^ ks[0], d0.y ^ ks[1], d0.z ^ ks[2], d0.w ^ ks[3]);
-            const uint4 r1 = make_uint4(d1.x ^ ks[4], d1.y ^ ks[5], d1.z ^ ks[6], d1.w ^ ks[7]);
-            const uint4 r2 = make_uint4(d2.x ^ ks[8], d2.y ^ ks[9], d2.z ^ ks[10], d2.w ^ ks[11]);
-            const uint4 r3 = make_uint4(d3.x ^ ks[12], d3.y ^ ks[13], d3.z ^ ks[14], d3.w ^ ks[15]);
-            uint4* dst = reinterpret_cast<uint4*>(out + off);
-            dst[0] = r0; dst[1] = r1; dst[2] = r2; dst[3] = r3;
-            uint4* cl = reinterpret_cast<uint4*>(ct_lds + off);
+            const u32x4 r0 = d0 ^ u32x4{ks[0], ks[1], ks[2], ks[3]};
+            const u32x4 r1 = d1 ^ u32x4{ks[4], ks[5], ks[6], ks[7]};
+            const u32x4 r2 = d2 ^ u32x4{ks[8], ks[9], ks[10], ks[11]};
+            const u32x4 r3 = d3 ^ u32x4{ks[12], ks[13], ks[14], ks[15]};
+            st16(out + off, r0);
+            st16(out + off + 16, r1);
+            st16(out + off + 32, r2);
+            st16(out + off + 48, r3);
             if constexpr (OPEN) {
-                cl[0] = d0; cl[1] = d1; cl[2] = d2; cl[3] = d3;
+                st16(ct_lds + off, d0);
+                st16(ct_lds + off + 16, d1);
+                st16(ct_lds + off + 32, d2);
+                st16(ct_lds + off + 48, d3);
             } else {
-                cl[0] = r0; cl[1] = r1; cl[2] = r2; cl[3] = r3;
+                st16(ct_lds + off, r0);
+                st16(ct_lds + off + 16, r1);
+                st16(ct_lds + off + 32, r2);
+                st16(ct_lds + off + 48, r3);
             }
         } else {
             // partial last block or misaligned record: byte granular
@@ -310,8 +400,13 @@ __global__ __launch_bounds__(256) void sg_aead_kernel(const KParams p) {
 
     // ---- MAC stream framing in LDS: ad || le64(|ad|) || ct || le64(|ct|) ----
     const uint32_t adlen = p.tls ? 13u : p.ad_len;
-    const uint32_t S = A - adlen - 8u;  // stream start
+    const uint32_t S = A - adlen - 8u;  // stream start, >= kZeroRegion
+    const MacGeom g = mac_geom(adlen, n);
     if (tid < 64u) {
+        const u32x4 zero = {0u, 0u, 0u, 0u};
+        st16(lds + 16u * tid, zero);  // [0, 2048): virtual blocks read zeros
+        st16(lds + 1024u + 16u * tid, zero);
+        if (kZeroRegion + tid < S) lds[kZeroRegion + tid] = 0;
         for (uint32_t i = tid; i < adlen + 8u; i += 64u) {
             uint8_t v;
             if (i < adlen)
@@ -320,77 +415,76 @@ __global__ __launch_bounds__(256) void sg_aead_kernel(const KParams p) {
                 v = (uint8_t)((uint64_t)adlen >> (8u * (i - adlen)));
             lds[S + i] = v;
         }
+        // suffix le64(n), then zeros to the end of the last block (+4 funnel bytes)
         if (tid < 8u) ct_lds[n + tid] = (uint8_t)((uint64_t)n >> (8u * tid));
+        else if (tid < 8u + 20u) ct_lds[n + tid] = 0;
     }
     __syncthreads();
     if (tid >= 64u) return;
 
     // ---- phase 2 (wave 0): Poly1305 ----------------------------------------
     const uint32_t* kr = p.ws + (uint64_t)rec * kKeyRecWords;
-    uint32_t pw[7][5];
-#pragma unroll
-    for (int k = 0; k < 7; ++k)
-#pragma unroll
-        for (int i = 0; i < 5; ++i) pw[k][i] = kr[kPowOff + 5 * k + i];
+    const uint32_t r0 = uniform(kr[kR32Off + 0]), r1 = uniform(kr[kR32Off + 1]);
+    const uint32_t r2 = uniform(kr[kR32Off + 2]), r3 = uniform(kr[kR32Off + 3]);
+    const uint32_t s1 = r1 + (r1 >> 2), s2 = r2 + (r2 >> 2), s3 = r3 + (r3 >> 2);
 
-    const uint32_t L = adlen + 16u + n;         // MAC stream length
-    const uint32_t B = (L + 15u) >> 4;          // MAC blocks
-    const uint32_t z = (64u - (B & 63u)) & 63u; // leading virtual zero blocks
-    const uint32_t J = (B + z) >> 6;
+    // lane t: virtual blocks [t*k, t*k + k); virtual block v is real iff v >= z
     const uint32_t sh = (S & 3u) * 8u;
+    const uint32_t v0 = tid * g.k;
+    uint32_t pos = S - 16u * g.z + 16u * v0;
     const uint32_t* l32 = reinterpret_cast<const uint32_t*>(lds);
-
-    F26 h = f26_zero();
-    for (uint32_t j = 0; j < J; ++j) {
-        const int32_t i = (int32_t)(tid + 64u * j) - (int32_t)z;
-        F26 c = f26_zero();
-        if (i >= 0) {
-            const uint32_t pos = S + 16u * (uint32_t)i;
-            const uint32_t q = pos >> 2;
-            const uint32_t a0 = l32[q], a1 = l32[q + 1], a2 = l32[q + 2], a3 = l32[q + 3], a4 = l32[q + 4];
-            uint32_t w0 = __builtin_amdgcn_alignbit(a1, a0, sh);
-            uint32_t w1 = __builtin_amdgcn_alignbit(a2, a1, sh);
-            uint32_t w2 = __builtin_amdgcn_alignbit(a3, a2, sh);
-            uint32_t w3 = __builtin_amdgcn_alignbit(a4, a3, sh);
-            uint32_t hibit = 1u << 24;  // 2^128 pad bit of a full block
-            const uint32_t rem = L - 16u * (uint32_t)i;
-            if (rem < 16u) {  // final partial block: zero-pad, pad bit at 8*rem (poly1305.rs:216-225)
-                hibit = 0u;
-                const uint32_t bit = 8u * rem;
-                uint32_t m0 = bit >= 32u ? ~0u : ((1u << bit) - 1u);
-                uint32_t m1 = bit >= 64u ? ~0u : (bit <= 32u ? 0u : ((1u << (bit - 32u)) - 1u));
-                uint32_t m2 = bit >= 96u ? ~0u : (bit <= 64u ? 0u : ((1u << (bit - 64u)) - 1u));
-                uint32_t m3 = bit <= 96u ? 0u : ((1u << (bit - 96u)) - 1u);
-                w0 &= m0; w1 &= m1; w2 &= m2; w3 &= m3;
-                const uint32_t fb = 1u << (bit & 31u);
-                const uint32_t fw = bit >> 5;
-                w0 |= fw == 0u ? fb : 0u;
-                w1 |= fw == 1u ? fb : 0u;
-                w2 |= fw == 2u ? fb : 0u;
-                w3 |= fw == 3u ? fb : 0u;
+    const uint32_t rem = g.L - 16u * (g.B - 1u);  // bytes in the final block, 1..16
+    H32 h = {0u, 0u, 0u, 0u, 0u};
+    for (uint32_t j = 0; j < g.k; ++j) {
+        const uint32_t q = pos >> 2;
+        const uint32_t a0 = l32[q], a1 = l32[q + 1], a2 = l32[q + 2], a3 = l32[q + 3], a4 = l32[q + 4];
+        uint32_t m0 = __builtin_amdgcn_alignbit(a1, a0, sh);
+        uint32_t m1 = __builtin_amdgcn_alignbit(a2, a1, sh);
+        uint32_t m2 = __builtin_amdgcn_alignbit(a3, a2, sh);
+        uint32_t m3 = __builtin_amdgcn_alignbit(a4, a3, sh);
+        uint32_t pad = (v0 + j >= g.z) ? 1u : 0u;  // 2^128 for a full real block
+        if (j + 1u == g.k && rem < 16u) {
+            // lane 63 holds the final, partial block: pad bit at 8 * rem
+            // (poly1305.rs:216-225; the bytes after the stream are zero)
+            if (tid == 63u) {
+                const uint32_t fb = 1u << (8u * (rem & 3u));
+                const uint32_t fw = rem >> 2;
+                m0 |= fw == 0u ? fb : 0u;
+                m1 |= fw == 1u ? fb : 0u;
+                m2 |= fw == 2u ? fb : 0u;
+                m3 |= fw == 3u ? fb : 0u;
+                pad = 0u;
             }
-            c = block_to_f26(w0, w1, w2, w3, hibit);
         }
-        h = (j == 0) ? c : mul_add(h, pw[6], c);  // h = h * r^64 + c
+        horner_step(h, m0, m1, m2, m3, pad, r0, r1, r2, r3, s1, s2, s3);
+        pos += 16u;
+    }
+    // radix 2^32 -> 2^26 for the tree (h < 2^131)
+    F26 f = words_to_f26(h.h0, h.h1, h.h2, h.h3, 0u);
+    f.v4 += h.h4 << 24;
+    {
+        const uint32_t c = f.v4 >> 26;
+        f.v4 &= M26;
+        f.v0 += c * 5u;
     }
     // combine lanes: after level l, lane t (t % 2^(l+1) == 0) holds
-    // sum_{u=t}^{t+2^(l+1)-1} h_u r^(t+2^(l+1)-1-u)
+    // sum_{u=t}^{t+2^(l+1)-1} h_u R^(t+2^(l+1)-1-u), R = r^k
 #pragma unroll
     for (int l = 0; l < 6; ++l) {
         const int d = 1 << l;
         F26 o;
-        o.v0 = __shfl_down(h.v0, d, 64);
-        o.v1 = __shfl_down(h.v1, d, 64);
-        o.v2 = __shfl_down(h.v2, d, 64);
-        o.v3 = __shfl_down(h.v3, d, 64);
-        o.v4 = __shfl_down(h.v4, d, 64);
-        h = mul_add(h, pw[l], o);
+        o.v0 = __shfl_down(f.v0, d, 64);
+        o.v1 = __shfl_down(f.v1, d, 64);
+        o.v2 = __shfl_down(f.v2, d, 64);
+        o.v3 = __shfl_down(f.v3, d, 64);
+        o.v4 = __shfl_down(f.v4, d, 64);
+        const uint32_t* R = kr + kPowOff + 5 * l;
+        f = mul_add(f, uniform(R[0]), uniform(R[1]), uniform(R[2]), uniform(R[3]), uniform(R[4]), o);
     }
     if (tid != 0) return;
-    h = mul_add(h, pw[0], f26_zero());  // * r
     uint32_t s[4] = {kr[kSOff + 0], kr[kSOff + 1], kr[kSOff + 2], kr[kSOff + 3]};
     uint32_t t[4];
-    tag_words(h, s, t);
+    tag_words(f, s, t);
 
     if constexpr (!OPEN) {
         uint8_t* tp = out + n;  // ct || tag (chacha20_poly1305.rs:55)
@@ -467,9 +561,14 @@ __global__ __launch_bounds__(256) void sg_compare_kernel(const uint8_t* a, uint6
 
 }  // namespace
 
-hipError_t launch_keying(const KParams& p, hipStream_t s) {
+uint32_t lds_ct_off(uint32_t adlen) { return kZeroRegion + ((adlen + 8u + 15u) & ~15u); }
+
+hipError_t launch_keying(const KParams& p, bool open, hipStream_t s) {
     const uint32_t grid = (p.count + 255u) / 256u;
-    hipLaunchKernelGGL(sg_keying_kernel, dim3(grid), dim3(256), 0, s, p);
+    if (open)
+        hipLaunchKernelGGL(sg_keying_kernel<true>, dim3(grid), dim3(256), 0, s, p);
+    else
+        hipLaunchKernelGGL(sg_keying_kernel<false>, dim3(grid), dim3(256), 0, s, p);
     return hipGetLastError();
 }
 
@@ -502,8 +601,9 @@ hipError_t launch_compare(const uint8_t* a, uint64_t sa, const uint8_t* b, uint6
 }
 
 const char* kernel_config() {
-    return "gfx950 sg_aead_kernel v1: 256 threads/record, lane=64B ChaCha block, "
-           "wave0 Poly1305 radix-2^26 strided-Horner(r^64)+6-level tree, keying pre-pass";
+    return "gfx950 sg_aead_kernel v2: 256 threads/record, lane=64B ChaCha block, "
+           "wave0 Poly1305 contiguous-chunk Horner radix-2^32 (clamped r) + 6-level r^(k*2^l) tree, "
+           "keying pre-pass";
 }
 
 }  // namespace sg
