@@ -34,8 +34,8 @@ METRIC = "GiB/s device-resident ChaCha20-Poly1305 over 16 KiB TLS records, 1/2/4
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--records", type=int, default=1 << 20, help="records per GPU (C1: 2^20)")
     ap.add_argument("--record-bytes", type=int, default=16384)
     ap.add_argument("--cpu-sample", type=int, default=4096, help="records in the CPU-baseline sample")
@@ -154,7 +154,7 @@ def main():
 
     # per-kernel device time with HIP events on the launch stream
     B.set_timing(True)
-    for _ in range(3):
+    for _ in range(5):
         step()
     tm = B.timing_read()
     B.set_timing(False)

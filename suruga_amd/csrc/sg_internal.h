@@ -8,13 +8,17 @@
 namespace sg {
 
 constexpr uint32_t kThreads = 256;        // one record per 256-thread workgroup
-constexpr uint32_t kKeyRecWords = 40;     // per-record keying output (u32 words)
+constexpr uint32_t kKeyRecWords = 96;     // per-record keying output (u32 words, 384 B)
 // keying record layout (u32 words): r[4] clamped Poly1305 r (radix 2^32),
-// s[4] (second half of keystream block 0), R[6][5] = r^(k*2^l), l = 0..5, in
-// radix 2^26 (k = MAC blocks per lane, see mac_geom in sg_kernels.hip), 2 pad.
+// s[4] (second half of keystream block 0), then with R = r^k (k = MAC blocks
+// per lane, see mac_geom in sg_kernels.hip), in radix 2^26:
+//   lo[8][5] = R^j       j = 0..7
+//   hi[8][5] = R^(8 i)   i = 0..7
+// so that MAC lane t = 8a + b scales its partial sum by R^(63-t) = hi[7-a] lo[7-b].
 constexpr uint32_t kR32Off = 0;
 constexpr uint32_t kSOff = 4;
-constexpr uint32_t kPowOff = 8;
+constexpr uint32_t kPowLoOff = 8;
+constexpr uint32_t kPowHiOff = 48;
 
 // Kernel parameters (passed by value as kernarg).
 struct KParams {

@@ -5,8 +5,8 @@
 //
 //   sg_keying_kernel   one lane per record: ChaCha20 block 0 -> Poly1305 key
 //                      (r clamped, s; chacha20_poly1305.rs:50,75,32-39,
-//                      poly1305.rs:197-203) and the six powers
-//                      r^(k*2^l), l = 0..5, that combine the MAC lanes.
+//                      poly1305.rs:197-203) and the 16 powers of r^k
+//                      that combine the MAC lanes.
 //   sg_aead_kernel<OPEN>
 //     phase 1, all 4 waves: lane t owns 64-byte data blocks t, t+256, ...;
 //       computes keystream block b+1 in registers (chacha20.rs:53-135),
@@ -17,9 +17,9 @@
 //       preceded by z zero "virtual" blocks (leading zeros do not change a
 //       Horner polynomial) so that B + z = 64k; lane t runs the reference's
 //       Horner step h = (h + c) * r (poly1305.rs:213-228) over its k
-//       contiguous blocks in radix 2^32 with the clamped r, and a 6-level
-//       shuffle tree with multipliers r^(k*2^l) (radix 2^26) sums
-//       h_t * r^(k*(63-t)).  Lane 0 reduces mod 2^130-5, adds s
+//       contiguous blocks in radix 2^32 with the clamped r; each lane then
+//       scales its sum by r^(k*(63-t)) (radix 2^26, powers from the keying
+//       record) and a shuffle reduction adds the 64 terms.  Lane 0 reduces mod 2^130-5, adds s
 //       (poly1305.rs:230-312) and seals (chacha20_poly1305.rs:55) or
 //       compares in constant time (:84-93) after decrypting
 //       unconditionally (:80-82).
@@ -117,6 +117,11 @@ __device__ __forceinline__ F26 mul_add(const F26 a, const uint32_t b0, const uin
 
 __device__ __forceinline__ F26 f26_zero() { return F26{0u, 0u, 0u, 0u, 0u}; }
 
+__device__ __forceinline__ void store_f26(uint32_t* p, const F26& x) {
+    p[0] = x.v0; p[1] = x.v1; p[2] = x.v2; p[3] = x.v3; p[4] = x.v4;
+}
+__device__ __forceinline__ F26 load_f26(const uint32_t* p) { return F26{p[0], p[1], p[2], p[3], p[4]}; }
+
 // Full carry: every limb < 2^26 (value < 2^130, not yet < p).
 __device__ __forceinline__ F26 carry_full(F26 h) {
 #pragma unroll
@@ -131,10 +136,28 @@ __device__ __forceinline__ F26 carry_full(F26 h) {
     return h;
 }
 
+// Strict normal form: every limb < 2^26 (value < 2^130), for limbs < 2^32.
+__device__ __forceinline__ F26 ripple_full(F26 h) {
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+        uint32_t c;
+        c = h.v0 >> 26; h.v0 &= M26; h.v1 += c;
+        c = h.v1 >> 26; h.v1 &= M26; h.v2 += c;
+        c = h.v2 >> 26; h.v2 &= M26; h.v3 += c;
+        c = h.v3 >> 26; h.v3 &= M26; h.v4 += c;
+        c = h.v4 >> 26; h.v4 &= M26; h.v0 += c * 5u;
+    }
+    // a second-pass fold implies v1..v4 wrapped to 0, so this cannot overflow v1
+    const uint32_t c = h.v0 >> 26;
+    h.v0 &= M26;
+    h.v1 += c;
+    return h;
+}
+
 // Canonical representative in [0, p): subtract p when h >= p, branch-free
 // (the role of Int1305::normalize, poly1305.rs:165-192).
 __device__ __forceinline__ F26 canonical(F26 h) {
-    h = carry_full(h);
+    h = ripple_full(h);
     uint32_t g0 = h.v0 + 5u, c = g0 >> 26; g0 &= M26;
     uint32_t g1 = h.v1 + c; c = g1 >> 26; g1 &= M26;
     uint32_t g2 = h.v2 + c; c = g2 >> 26; g2 &= M26;
@@ -274,42 +297,68 @@ __device__ __forceinline__ uint32_t record_len(const KParams& p, uint32_t rec) {
 // ---------------------------------------------------------------------------
 // Keying pre-pass: one lane per record.
 // ---------------------------------------------------------------------------
+// The 64 records of a wave are staged in LDS (row stride 97 words: no bank
+// conflicts) and leave as one contiguous 24 KiB run of 16-byte stores; one
+// lane writing its own 384-byte record would touch 64 cache lines per store.
+constexpr uint32_t kKeyingThreads = 64;
+constexpr uint32_t kKeyLdsStride = kKeyRecWords + 1;
+
 template <bool OPEN>
-__global__ __launch_bounds__(256) void sg_keying_kernel(const KParams p) {
-    const uint32_t rec = blockIdx.x * blockDim.x + threadIdx.x;
-    if (rec >= p.count) return;
-    const uint32_t len = record_len(p, rec);
-    const uint32_t n = OPEN ? (len >= 16u ? len - 16u : 0u) : len;
-    const RecKey rk = record_key(p, rec);
-    uint32_t ks[16];
-    chacha_block(ks, rk.k, 0u, rk.n14, rk.n15);  // block 0 -> poly key (chacha20_poly1305.rs:50)
-    // r = clamp(pk[0..16]) (poly1305.rs:197-203), s = pk[16..32]
-    const uint32_t r0 = ks[0] & 0x0fffffffu, r1 = ks[1] & 0x0ffffffcu;
-    const uint32_t r2 = ks[2] & 0x0ffffffcu, r3 = ks[3] & 0x0ffffffcu;
-    uint32_t* out = p.ws + (uint64_t)rec * kKeyRecWords;
-    out[kR32Off + 0] = r0;
-    out[kR32Off + 1] = r1;
-    out[kR32Off + 2] = r2;
-    out[kR32Off + 3] = r3;
-    out[kSOff + 0] = ks[4];
-    out[kSOff + 1] = ks[5];
-    out[kSOff + 2] = ks[6];
-    out[kSOff + 3] = ks[7];
-    // R = r^k by square-and-multiply, then R^(2^l) for the lane-combining tree
-    const MacGeom g = mac_geom(p.tls ? 13u : p.ad_len, n);
-    const F26 r = words_to_f26(r0, r1, r2, r3, 0u);
-    F26 R = r;
-    for (int bit = 30 - __builtin_clz(g.k); bit >= 0; --bit) {
-        R = carry_full(mul_add(R, R.v0, R.v1, R.v2, R.v3, R.v4, f26_zero()));
-        if ((g.k >> bit) & 1u) R = carry_full(mul_add(R, r.v0, r.v1, r.v2, r.v3, r.v4, f26_zero()));
+__global__ __launch_bounds__(64) void sg_keying_kernel(const KParams p) {
+    __shared__ uint32_t stage[kKeyingThreads * kKeyLdsStride];
+    const uint32_t lane = threadIdx.x;
+    const uint32_t rec0 = blockIdx.x * kKeyingThreads;
+    const uint32_t rec = rec0 + lane;
+    uint32_t* out = stage + lane * kKeyLdsStride;
+    if (rec < p.count) {
+        const uint32_t len = record_len(p, rec);
+        const uint32_t n = OPEN ? (len >= 16u ? len - 16u : 0u) : len;
+        const RecKey rk = record_key(p, rec);
+        uint32_t ks[16];
+        chacha_block(ks, rk.k, 0u, rk.n14, rk.n15);  // block 0 -> poly key (chacha20_poly1305.rs:50)
+        // r = clamp(pk[0..16]) (poly1305.rs:197-203), s = pk[16..32]
+        const uint32_t r0 = ks[0] & 0x0fffffffu, r1 = ks[1] & 0x0ffffffcu;
+        const uint32_t r2 = ks[2] & 0x0ffffffcu, r3 = ks[3] & 0x0ffffffcu;
+        out[kR32Off + 0] = r0;
+        out[kR32Off + 1] = r1;
+        out[kR32Off + 2] = r2;
+        out[kR32Off + 3] = r3;
+        out[kSOff + 0] = ks[4];
+        out[kSOff + 1] = ks[5];
+        out[kSOff + 2] = ks[6];
+        out[kSOff + 3] = ks[7];
+        // R = r^k by square-and-multiply; then R^0..R^7 and R^0, R^8, .., R^56.
+        // mul_add outputs are valid multipliers as they stand (limb 1 may exceed
+        // 2^26 by < 2^8), so no extra carry passes are needed here.
+        const MacGeom g = mac_geom(p.tls ? 13u : p.ad_len, n);
+        const F26 r = words_to_f26(r0, r1, r2, r3, 0u);
+        F26 R = r;
+        for (int bit = 30 - __builtin_clz(g.k); bit >= 0; --bit) {
+            R = mul_add(R, R.v0, R.v1, R.v2, R.v3, R.v4, f26_zero());
+            if ((g.k >> bit) & 1u) R = mul_add(R, r.v0, r.v1, r.v2, r.v3, r.v4, f26_zero());
+        }
+        F26 x = F26{1u, 0u, 0u, 0u, 0u};
+        for (int j = 0; j < 8; ++j) {  // lo[j] = R^j
+            store_f26(out + kPowLoOff + 5 * j, x);
+            x = mul_add(x, R.v0, R.v1, R.v2, R.v3, R.v4, f26_zero());
+        }
+        const F26 R8 = x;
+        x = F26{1u, 0u, 0u, 0u, 0u};
+        for (int i = 0; i < 8; ++i) {  // hi[i] = R^(8 i)
+            store_f26(out + kPowHiOff + 5 * i, x);
+            if (i < 7) x = mul_add(x, R8.v0, R8.v1, R8.v2, R8.v3, R8.v4, f26_zero());
+        }
     }
-    for (int l = 0; l < 6; ++l) {
-        out[kPowOff + 5 * l + 0] = R.v0;
-        out[kPowOff + 5 * l + 1] = R.v1;
-        out[kPowOff + 5 * l + 2] = R.v2;
-        out[kPowOff + 5 * l + 3] = R.v3;
-        out[kPowOff + 5 * l + 4] = R.v4;
-        if (l < 5) R = carry_full(mul_add(R, R.v0, R.v1, R.v2, R.v3, R.v4, f26_zero()));
+    __syncthreads();
+    // coalesced flush: the wave's records are contiguous in the workspace
+    const uint32_t nrec = p.count - rec0 < kKeyingThreads ? p.count - rec0 : kKeyingThreads;
+    u32x4* dst = reinterpret_cast<u32x4*>(p.ws + (uint64_t)rec0 * kKeyRecWords);
+    const uint32_t nvec = nrec * (kKeyRecWords / 4u);
+    for (uint32_t v = lane; v < nvec; v += kKeyingThreads) {
+        const uint32_t w = 4u * v;
+        const uint32_t rr = w / kKeyRecWords, c = w - rr * kKeyRecWords;
+        const uint32_t* src = stage + rr * kKeyLdsStride + c;
+        dst[v] = u32x4{src[0], src[1], src[2], src[3]};
     }
 }
 
@@ -467,19 +516,32 @@ __global__ __launch_bounds__(256) void sg_aead_kernel(const KParams p) {
         f.v4 &= M26;
         f.v0 += c * 5u;
     }
-    // combine lanes: after level l, lane t (t % 2^(l+1) == 0) holds
-    // sum_{u=t}^{t+2^(l+1)-1} h_u R^(t+2^(l+1)-1-u), R = r^k
+    // combine lanes: total = sum_t h_t R^(63-t), R = r^k.  Lane t = 8a + b
+    // scales by R^(63-t) = hi[7-a] * lo[7-b] (keying record), then the 64
+    // scaled values are summed limb-wise with shuffles.
+    {
+        const F26 plo = load_f26(kr + kPowLoOff + 5u * (7u - (tid & 7u)));
+        const F26 phi = load_f26(kr + kPowHiOff + 5u * (7u - (tid >> 3)));
+        const F26 P = mul_add(phi, plo.v0, plo.v1, plo.v2, plo.v3, plo.v4, f26_zero());
+        f = carry_full(mul_add(f, P.v0, P.v1, P.v2, P.v3, P.v4, f26_zero()));
+    }
+    // limbs < 2^26: 32 of them sum below 2^31, so carry once before the last level
 #pragma unroll
     for (int l = 0; l < 6; ++l) {
+        if (l == 5) {
+            uint32_t c;
+            c = f.v0 >> 26; f.v0 &= M26; f.v1 += c;
+            c = f.v1 >> 26; f.v1 &= M26; f.v2 += c;
+            c = f.v2 >> 26; f.v2 &= M26; f.v3 += c;
+            c = f.v3 >> 26; f.v3 &= M26; f.v4 += c;
+            c = f.v4 >> 26; f.v4 &= M26; f.v0 += c * 5u;
+        }
         const int d = 1 << l;
-        F26 o;
-        o.v0 = __shfl_down(f.v0, d, 64);
-        o.v1 = __shfl_down(f.v1, d, 64);
-        o.v2 = __shfl_down(f.v2, d, 64);
-        o.v3 = __shfl_down(f.v3, d, 64);
-        o.v4 = __shfl_down(f.v4, d, 64);
-        const uint32_t* R = kr + kPowOff + 5 * l;
-        f = mul_add(f, uniform(R[0]), uniform(R[1]), uniform(R[2]), uniform(R[3]), uniform(R[4]), o);
+        f.v0 += __shfl_xor(f.v0, d, 64);
+        f.v1 += __shfl_xor(f.v1, d, 64);
+        f.v2 += __shfl_xor(f.v2, d, 64);
+        f.v3 += __shfl_xor(f.v3, d, 64);
+        f.v4 += __shfl_xor(f.v4, d, 64);
     }
     if (tid != 0) return;
     uint32_t s[4] = {kr[kSOff + 0], kr[kSOff + 1], kr[kSOff + 2], kr[kSOff + 3]};
@@ -564,11 +626,11 @@ __global__ __launch_bounds__(256) void sg_compare_kernel(const uint8_t* a, uint6
 uint32_t lds_ct_off(uint32_t adlen) { return kZeroRegion + ((adlen + 8u + 15u) & ~15u); }
 
 hipError_t launch_keying(const KParams& p, bool open, hipStream_t s) {
-    const uint32_t grid = (p.count + 255u) / 256u;
+    const uint32_t grid = (p.count + kKeyingThreads - 1u) / kKeyingThreads;
     if (open)
-        hipLaunchKernelGGL(sg_keying_kernel<true>, dim3(grid), dim3(256), 0, s, p);
+        hipLaunchKernelGGL(sg_keying_kernel<true>, dim3(grid), dim3(kKeyingThreads), 0, s, p);
     else
-        hipLaunchKernelGGL(sg_keying_kernel<false>, dim3(grid), dim3(256), 0, s, p);
+        hipLaunchKernelGGL(sg_keying_kernel<false>, dim3(grid), dim3(kKeyingThreads), 0, s, p);
     return hipGetLastError();
 }
 
@@ -602,7 +664,7 @@ hipError_t launch_compare(const uint8_t* a, uint64_t sa, const uint8_t* b, uint6
 
 const char* kernel_config() {
     return "gfx950 sg_aead_kernel v2: 256 threads/record, lane=64B ChaCha block, "
-           "wave0 Poly1305 contiguous-chunk Horner radix-2^32 (clamped r) + 6-level r^(k*2^l) tree, "
+           "wave0 Poly1305 contiguous-chunk Horner radix-2^32 (clamped r) + per-lane r^(k(63-t)) scale + shuffle sum, "
            "keying pre-pass";
 }
 
