@@ -36,6 +36,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", choices=["c1", "c2"], default="c1",
+                    help="c1: 16 KiB records, one key (the metric's config); c2: Zipf 64 B-16 KiB, 256 keys")
     ap.add_argument("--records", type=int, default=1 << 20, help="records per GPU (C1: 2^20)")
     ap.add_argument("--record-bytes", type=int, default=16384)
     ap.add_argument("--cpu-sample", type=int, default=4096, help="records in the CPU-baseline sample")
@@ -108,18 +110,51 @@ def main():
         _build.build_library()
     n, count = args.record_bytes, args.records
     seq0 = rank * count
-    keys = torch.tensor(list(KEY), dtype=torch.uint8, device=dev).view(1, 32)
-    pt = torch.empty(count * n, dtype=torch.uint8, device=dev)
-    ct = torch.empty(count * (n + 16), dtype=torch.uint8, device=dev)
-    back = torch.empty(count * n, dtype=torch.uint8, device=dev)
-    status = torch.empty(count, dtype=torch.uint8, device=dev)
-    ws = torch.empty(B.workspace_size(count), dtype=torch.uint8, device=dev)
-    B.fill_records(pt, n, n, count, SEED, j0=seq0)
     stream = torch.cuda.current_stream(dev)
-    seal_b = B.Batch(count=count, keys=keys, inp=pt, out=ct, uniform_len=n, in_stride=n, out_stride=n + 16,
-                     seq0=seq0, workspace=ws, stream=stream)
-    open_b = B.Batch(count=count, keys=keys, inp=ct, out=back, uniform_len=n + 16, in_stride=n + 16,
-                     out_stride=n, seq0=seq0, status=status, workspace=ws, stream=stream)
+    ws = torch.empty(B.workspace_size(count), dtype=torch.uint8, device=dev)
+    status = torch.empty(count, dtype=torch.uint8, device=dev)
+    if args.workload == "c1":
+        keys = torch.tensor(list(KEY), dtype=torch.uint8, device=dev).view(1, 32)
+        pt = torch.empty(count * n, dtype=torch.uint8, device=dev)
+        ct = torch.empty(count * (n + 16), dtype=torch.uint8, device=dev)
+        back = torch.empty(count * n, dtype=torch.uint8, device=dev)
+        B.fill_records(pt, n, n, count, SEED, j0=seq0)
+        seal_b = B.Batch(count=count, keys=keys, inp=pt, out=ct, uniform_len=n, in_stride=n, out_stride=n + 16,
+                         seq0=seq0, workspace=ws, stream=stream)
+        open_b = B.Batch(count=count, keys=keys, inp=ct, out=back, uniform_len=n + 16, in_stride=n + 16,
+                         out_stride=n, seq0=seq0, status=status, workspace=ws, stream=stream)
+        payload_per_step = 2 * count * n
+        alg = {"seal": (2 * n + 69) * count, "open": (2 * n + 70) * count}
+        cfg = {"workload": f"C1: {count} x {n} B TLS records per GPU, one key, sequential seq, seal then open, "
+                           "device-resident", "records_per_gpu": count, "record_bytes": n}
+        cmp_args = (pt, n, back, n, n, count)
+    else:
+        import numpy as np
+
+        from suruga_amd import workloads as W
+
+        lay = W.c2_layout(count)
+        t64 = lambda a: torch.from_numpy(a.view(np.int64)).to(dev)
+        t32 = lambda a: torch.from_numpy(a.view(np.int32)).to(dev)
+        keys = torch.tensor(list(lay.keys), dtype=torch.uint8, device=dev).view(-1, 32)
+        pt = torch.empty(lay.pt_bytes, dtype=torch.uint8, device=dev)
+        ct = torch.empty(lay.ct_bytes, dtype=torch.uint8, device=dev)
+        back = torch.empty(lay.pt_bytes, dtype=torch.uint8, device=dev)
+        B.fill_records(pt, 0, lay.pt_bytes, 1, SEED, j0=seq0)
+        lens, olens = t32(lay.lens), t32(lay.lens + 16)
+        in_off, out_off, kidx = t64(lay.in_off), t64(lay.out_off), t32(lay.key_index)
+        seqs = t64(lay.seq + np.uint64(seq0 // 256))
+        maxl = int(lay.lens.max())
+        seal_b = B.Batch(count=count, keys=keys, inp=pt, out=ct, lens=lens, max_len=maxl, in_off=in_off,
+                         out_off=out_off, key_index=kidx, seq=seqs, workspace=ws, stream=stream)
+        open_b = B.Batch(count=count, keys=keys, inp=ct, out=back, lens=olens, max_len=maxl + 16, in_off=out_off,
+                         out_off=in_off, key_index=kidx, seq=seqs, status=status, workspace=ws, stream=stream)
+        payload_per_step = 2 * lay.payload
+        alg = {"seal": 2 * lay.payload + 69 * count, "open": 2 * lay.payload + 70 * count}
+        cfg = {"workload": f"C2: {count} TLS records per GPU, Zipf(1.1) sizes 64 B-16 KiB (mean "
+                           f"{lay.payload / count:.0f} B), 256 connection keys, seal then open, device-resident",
+                           "records_per_gpu": count, "record_bytes": "zipf"}
+        cmp_args = (pt, 64, back, 64, 64, lay.pt_bytes // 64)  # 64-byte granules
     seal_c, open_c = seal_b.to_c(), open_b.to_c()
     lib = B.N.load()
     import ctypes as C
@@ -148,7 +183,7 @@ def main():
 
     # correctness of the last step (outside the timed region)
     mism = torch.zeros(1, dtype=torch.int64, device=dev)
-    B.compare_records(pt, n, back, n, n, count, mism, stream=stream)
+    B.compare_records(*cmp_args, mism, stream=stream)
     bad_status = int((status != 0).sum().item())
     roundtrip_ok = int(mism.item()) == 0 and bad_status == 0
 
@@ -159,15 +194,14 @@ def main():
     tm = B.timing_read()
     B.set_timing(False)
 
-    payload = 2 * count * n * args.steps * world  # seal + open plaintext bytes, all ranks
+    payload = payload_per_step * args.steps * world  # seal + open plaintext bytes, all ranks
     value = payload / elapsed / 2**30
     ms_per_step = elapsed / args.steps * 1e3
 
     # dominant kernel's roofline (algorithmic bytes per launch):
     # seal R+W = 2n + 69 per record, open = 2n + 70
     dom = "open" if tm["open_ms"] >= tm["seal_ms"] else "seal"
-    per_rec = 2 * n + (70 if dom == "open" else 69)
-    alg_bytes = per_rec * count
+    alg_bytes = alg[dom]
     dom_ms = tm[f"{dom}_ms"]
     achieved = alg_bytes / (dom_ms * 1e-3) / 1e9
     traffic = None
@@ -175,30 +209,28 @@ def main():
     if tp.exists():
         try:
             tj = json.loads(tp.read_text())
-            if tj.get("records") == count and tj.get("record_bytes") == n:
+            if tj.get("records") == count and tj.get("record_bytes") == cfg["record_bytes"]:
                 traffic = tj.get(f"{dom}_bytes_per_launch")
         except (ValueError, OSError):
             traffic = None
 
     if rank == 0:
         cpu = None
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and args.workload == "c1":
             cpu = cpu_baseline(args, n)
         line = {
             "metric": METRIC, "value": round(value, 3), "unit": "GiB/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
             "data": "synthetic (splitmix64 records generated on device)",
-            "config": {"workload": f"C1: {count} x {n} B TLS records per GPU, one key, sequential seq, "
-                                   "seal then open, device-resident",
-                       "records_per_gpu": count, "record_bytes": n, "parallelism": f"record-shard x{world}",
-                       "kernels": lib.sg_build_info().decode()},
+            "config": dict(cfg, parallelism=f"record-shard x{world}", kernels=lib.sg_build_info().decode()),
             "roofline": {"bound": "hbm", "kernel": f"sg_aead_kernel<{'OPEN' if dom == 'open' else 'SEAL'}>",
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "alg_bytes_per_launch": alg_bytes, "avg_launch_ms": round(dom_ms, 4)},
             "kernel_ms": {"seal": round(tm["seal_ms"], 4), "open": round(tm["open_ms"], 4),
                           "keying": round(tm["keying_ms"], 4)},
+            "records_per_s": round(count * world * args.steps / elapsed, 1),
             "correct": roundtrip_ok,
             "cpu_baseline": cpu,
         }

@@ -182,9 +182,11 @@ int run_batch(const sg_batch* b, bool open) {
     p.ad_len = p.tls ? 13u : b->ad_len;
     p.ad_stride = b->ad_stride;
     p.tls_hdr = (uint32_t)b->content_type | ((uint32_t)b->ver_major << 8) | ((uint32_t)b->ver_minor << 16);
-    p.lds_ct_off = sg::lds_ct_off(p.ad_len);
     const uint32_t maxl = b->len ? b->max_len : b->uniform_len;
-    const uint32_t lds = sg::lds_bytes(p.lds_ct_off, maxl);
+    const uint32_t max_n = open ? (maxl >= 16u ? maxl - 16u : 0u) : maxl;
+    const bool uniform = !b->len || sg::size_class(max_n) == 0u;
+    uint32_t* lists = p.ws + (size_t)b->count * sg::kKeyRecWords;
+    uint32_t* counts = lists + (uint64_t)sg::kNumClasses * b->count;
 
     hipEvent_t e[4] = {nullptr, nullptr, nullptr, nullptr};
     if (g_timing)
@@ -195,7 +197,7 @@ int run_batch(const sg_batch* b, bool open) {
         SG_HIP(hipEventRecord(e[1], s));
         SG_HIP(hipEventRecord(e[2], s));
     }
-    SG_HIP(open ? sg::launch_open(p, lds, s) : sg::launch_seal(p, lds, s));
+    SG_HIP(sg::launch_aead(p, open, max_n, uniform, lists, counts, s));
     if (g_timing) {
         SG_HIP(hipEventRecord(e[3], s));
         g_timed.push_back({e[0], e[1], 0});
@@ -231,7 +233,10 @@ size_t sg_mac_len(void) { return SG_MAC_LEN; }
 int sg_abi_version(void) { return SG_ABI_VERSION; }
 const char* sg_last_error(void) { return g_err.c_str(); }
 const char* sg_build_info(void) { return sg::kernel_config(); }
-size_t sg_workspace_size(uint32_t count) { return (size_t)count * sg::kKeyRecWords * 4u; }
+size_t sg_workspace_size(uint32_t count) {
+    // keying records, one list per size class, four list counters
+    return (size_t)count * (sg::kKeyRecWords + sg::kNumClasses) * 4u + 16u;
+}
 
 sg_ctx* sg_ctx_new(const uint8_t key[32], int device) {
     if (!key) {

@@ -36,28 +36,42 @@ struct KParams {
     uint64_t out_stride;
     const uint32_t* len;
     uint8_t* status;
-    uint32_t* ws;            // count * kKeyRecWords
+    uint32_t* ws;            // count * kKeyRecWords (keying records)
     uint32_t uniform_len;
     uint32_t count;
     uint32_t ad_len;         // explicit mode
     uint32_t ad_stride;
     uint32_t tls;            // 1 = SG_BATCH_TLS
     uint32_t tls_hdr;        // content_type | major << 8 | minor << 16
-    uint32_t lds_ct_off;     // LDS offset of ciphertext byte 0 (16-aligned)
+    uint32_t lds_rec_bytes;  // LDS bytes per record slot of the launched size class
     uint32_t pad;
 };
 
-// LDS offset of ciphertext byte 0 (16-aligned, after the zero region and the
-// ad || le64(adlen) prefix), and the LDS bytes one workgroup needs for records
-// of at most max_n payload bytes.
-uint32_t lds_ct_off(uint32_t adlen);
-inline uint32_t lds_bytes(uint32_t ct_off, uint32_t max_n) {
-    return ct_off + ((max_n + 63) & ~63u) + 64;
+// Size classes of the AEAD kernel: lanes per record L = 16 (n <= 1 KiB),
+// 64 (n <= 4 KiB), 128 (n <= 8 KiB) or 256; MAC lanes PL = min(L, 64).
+// Records of mixed sizes are bucketed on the device (sg_classify_kernel).
+constexpr uint32_t kNumClasses = 4;
+constexpr uint32_t kClass0Max = 1024;
+constexpr uint32_t kClass1Max = 4096;
+constexpr uint32_t kClass2Max = 8192;
+constexpr uint32_t kListGridPerCU = 8;   // workgroups per CU for list-driven launches
+
+__host__ __device__ inline uint32_t size_class(uint32_t n) {
+    return n <= kClass0Max ? 0u : (n <= kClass1Max ? 1u : (n <= kClass2Max ? 2u : 3u));
+}
+// LDS bytes of one record slot: zero region (16 bytes x max virtual blocks
+// 2*PL) | ad || le64 (16-rounded) | ct (64-rounded) | le64(n) + zeros + funnel slack
+__host__ __device__ inline uint32_t lds_rec_bytes(uint32_t cls, uint32_t adlen, uint32_t max_n) {
+    const uint32_t PL = cls == 0 ? 16u : 64u;
+    return 32u * PL + ((adlen + 8u + 15u) & ~15u) + ((max_n + 63u) & ~63u) + 64u;
 }
 
 hipError_t launch_keying(const KParams& p, bool open, hipStream_t s);
-hipError_t launch_seal(const KParams& p, uint32_t lds, hipStream_t s);
-hipError_t launch_open(const KParams& p, uint32_t lds, hipStream_t s);
+// Seal/open launch.  uniform: every record is in size_class(max_n) (direct
+// launch); otherwise classify into lists[kNumClasses][count] / counts[4] and
+// launch per class.
+hipError_t launch_aead(const KParams& p, bool open, uint32_t max_n, bool uniform, uint32_t* lists,
+                       uint32_t* counts, hipStream_t s);
 hipError_t launch_fill(uint8_t* buf, uint64_t stride, uint32_t len, uint32_t count, uint64_t seed,
                        uint64_t j0, hipStream_t s);
 hipError_t launch_compare(const uint8_t* a, uint64_t sa, const uint8_t* b, uint64_t sb, uint32_t len,

@@ -34,7 +34,6 @@ namespace sg {
 namespace {
 
 constexpr uint32_t M26 = (1u << 26) - 1;
-constexpr uint32_t kZeroRegion = 2048;  // LDS bytes of zeros in front of the MAC stream
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -248,19 +247,24 @@ __device__ __forceinline__ void horner_step(H32& h, uint32_t m0, uint32_t m1, ui
 }
 
 // MAC geometry: stream length L, blocks B, lane chunk k (odd: spreads the
-// lanes' LDS reads over banks), leading virtual zero blocks z = 64k - B.
+// lanes' LDS reads over banks), leading virtual zero blocks z = PL*k - B, for
+// PL MAC lanes per record.
 struct MacGeom {
     uint32_t L, B, k, z;
 };
-__device__ __forceinline__ MacGeom mac_geom(uint32_t adlen, uint32_t n) {
+__device__ __forceinline__ MacGeom mac_geom(uint32_t adlen, uint32_t n, uint32_t PL) {
     MacGeom g;
     g.L = adlen + 16u + n;
     g.B = (g.L + 15u) >> 4;
-    g.k = (g.B + 63u) >> 6;
+    g.k = (g.B + PL - 1u) / PL;
     g.k |= 1u;
-    g.z = 64u * g.k - g.B;
+    g.z = PL * g.k - g.B;
     return g;
 }
+
+// MAC lanes per record, a function of the payload length only so that the
+// keying kernel and every AEAD size class agree on k (see size_class).
+__device__ __forceinline__ uint32_t mac_lanes(uint32_t n) { return n <= kClass0Max ? 16u : 64u; }
 
 // Per-record parameters shared by the keying and AEAD kernels.
 struct RecKey {
@@ -330,7 +334,7 @@ __global__ __launch_bounds__(64) void sg_keying_kernel(const KParams p) {
         // R = r^k by square-and-multiply; then R^0..R^7 and R^0, R^8, .., R^56.
         // mul_add outputs are valid multipliers as they stand (limb 1 may exceed
         // 2^26 by < 2^8), so no extra carry passes are needed here.
-        const MacGeom g = mac_geom(p.tls ? 13u : p.ad_len, n);
+        const MacGeom g = mac_geom(p.tls ? 13u : p.ad_len, n, mac_lanes(n));
         const F26 r = words_to_f26(r0, r1, r2, r3, 0u);
         F26 R = r;
         for (int bit = 30 - __builtin_clz(g.k); bit >= 0; --bit) {
@@ -374,112 +378,123 @@ __device__ __forceinline__ uint8_t tls_ad_byte(uint64_t seq, uint32_t hdr, uint3
 __device__ __forceinline__ uint32_t uniform(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
 
 // ---------------------------------------------------------------------------
-// Fused seal / open: one record per workgroup.
-// LDS: [0, S) zeros | S: ad | le64(adlen) | A: ct (n) | le64(n) | zeros
+// Fused seal / open.  A 256-thread workgroup serves RPW = 256 / L records with
+// L lanes each (size classes: L = 16 for n <= 1 KiB, 64 for n <= 4 KiB, 256
+// otherwise); PL = min(L, 64) of them run the MAC.  Per record, in LDS:
+//   [0, S) zeros | S: ad | le64(adlen) | A: ct (n) | le64(n) | zeros
 // ---------------------------------------------------------------------------
-template <bool OPEN>
-__global__ __launch_bounds__(256) void sg_aead_kernel(const KParams p) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    const uint32_t rec = blockIdx.x;
-    const uint32_t tid = threadIdx.x;
-
-    const uint32_t len = record_len(p, rec);
-    uint32_t n = len;
-    if constexpr (OPEN) {
-        if (len < 16u) {  // chacha20_poly1305.rs:68-70 "message too short"
-            if (tid == 0) p.status[rec] = 2u;
-            return;
-        }
-        n = len - 16u;
-    }
-    const uint8_t* in = p.in + (p.in_off ? p.in_off[rec] : p.in_stride * rec);
-    uint8_t* out = p.out + (p.out_off ? p.out_off[rec] : p.out_stride * rec);
-    const RecKey rk = record_key(p, rec);
-    const uint32_t A = p.lds_ct_off;
-    uint8_t* ct_lds = lds + A;
-
-    // ---- phase 1: keystream XOR, 64 bytes per lane-block ------------------
-    const bool vec_ok = (((uintptr_t)in | (uintptr_t)out) & 15u) == 0u;
-    const uint32_t nblocks = (n + 63u) >> 6;
-    for (uint32_t b = tid; b < nblocks; b += kThreads) {
-        const uint32_t off = b << 6;
-        if (vec_ok && off + 64u <= n) {
-            const u32x4 d0 = ld16(in + off), d1 = ld16(in + off + 16);
-            const u32x4 d2 = ld16(in + off + 32), d3 = ld16(in + off + 48);
-            uint32_t ks[16];
-            chacha_block(ks, rk.k, b + 1u, rk.n14, rk.n15);  // data uses blocks 1.. (chacha20_poly1305.rs:52)
-            const u32x4 r0 = d0 ^ u32x4{ks[0], ks[1], ks[2], ks[3]};
-            const u32x4 r1 = d1 ^ u32x4{ks[4], ks[5], ks[6], ks[7]};
-            const u32x4 r2 = d2 ^ u32x4{ks[8], ks[9], ks[10], ks[11]};
-            const u32x4 r3 = d3 ^ u32x4{ks[12], ks[13], ks[14], ks[15]};
-            st16(out + off, r0);
-            st16(out + off + 16, r1);
-            st16(out + off + 32, r2);
-            st16(out + off + 48, r3);
-            if constexpr (OPEN) {
-                st16(ct_lds + off, d0);
-                st16(ct_lds + off + 16, d1);
-                st16(ct_lds + off + 32, d2);
-                st16(ct_lds + off + 48, d3);
-            } else {
-                st16(ct_lds + off, r0);
-                st16(ct_lds + off + 16, r1);
-                st16(ct_lds + off + 32, r2);
-                st16(ct_lds + off + 48, r3);
+template <bool OPEN, uint32_t L>
+__device__ __forceinline__ void aead_record(const KParams& p, const uint32_t rec, const bool active,
+                                            uint8_t* lds, const uint32_t t) {
+    constexpr uint32_t PL = L < 64u ? L : 64u;
+    constexpr uint32_t Z = 32u * PL;  // zero bytes in front: 16 * max z
+    uint32_t n = 0;
+    bool work = active;
+    const uint32_t len = active ? record_len(p, rec) : 0u;
+    if (active) {
+        n = len;
+        if constexpr (OPEN) {
+            if (len < 16u) {  // chacha20_poly1305.rs:68-70 "message too short"
+                if (t == 0) p.status[rec] = 2u;
+                work = false;
             }
-        } else {
-            // partial last block or misaligned record: byte granular
-            uint32_t ks[16];
-            chacha_block(ks, rk.k, b + 1u, rk.n14, rk.n15);
+            n = len - 16u;
+        }
+    }
+    const uint8_t* in = nullptr;
+    uint8_t* out = nullptr;
+    RecKey rk = {};
+    const uint32_t adlen = p.tls ? 13u : p.ad_len;
+    const uint32_t A = Z + ((adlen + 8u + 15u) & ~15u);
+    const uint32_t S = A - adlen - 8u;  // stream start, >= Z
+    uint8_t* ct_lds = lds + A;
+    if (work) {
+        in = p.in + (p.in_off ? p.in_off[rec] : p.in_stride * rec);
+        out = p.out + (p.out_off ? p.out_off[rec] : p.out_stride * rec);
+        rk = record_key(p, rec);
+
+        // ---- phase 1: keystream XOR, 64 bytes per lane-block ----------------
+        const bool vec_ok = (((uintptr_t)in | (uintptr_t)out) & 15u) == 0u;
+        const uint32_t nblocks = (n + 63u) >> 6;
+        for (uint32_t b = t; b < nblocks; b += L) {
+            const uint32_t off = b << 6;
+            if (vec_ok && off + 64u <= n) {
+                const u32x4 d0 = ld16(in + off), d1 = ld16(in + off + 16);
+                const u32x4 d2 = ld16(in + off + 32), d3 = ld16(in + off + 48);
+                uint32_t ks[16];
+                chacha_block(ks, rk.k, b + 1u, rk.n14, rk.n15);  // data uses blocks 1.. (chacha20_poly1305.rs:52)
+                const u32x4 r0 = d0 ^ u32x4{ks[0], ks[1], ks[2], ks[3]};
+                const u32x4 r1 = d1 ^ u32x4{ks[4], ks[5], ks[6], ks[7]};
+                const u32x4 r2 = d2 ^ u32x4{ks[8], ks[9], ks[10], ks[11]};
+                const u32x4 r3 = d3 ^ u32x4{ks[12], ks[13], ks[14], ks[15]};
+                st16(out + off, r0);
+                st16(out + off + 16, r1);
+                st16(out + off + 32, r2);
+                st16(out + off + 48, r3);
+                if constexpr (OPEN) {
+                    st16(ct_lds + off, d0);
+                    st16(ct_lds + off + 16, d1);
+                    st16(ct_lds + off + 32, d2);
+                    st16(ct_lds + off + 48, d3);
+                } else {
+                    st16(ct_lds + off, r0);
+                    st16(ct_lds + off + 16, r1);
+                    st16(ct_lds + off + 32, r2);
+                    st16(ct_lds + off + 48, r3);
+                }
+            } else {
+                // partial last block or misaligned record: byte granular
+                uint32_t ks[16];
+                chacha_block(ks, rk.k, b + 1u, rk.n14, rk.n15);
 #pragma unroll
-            for (uint32_t w = 0; w < 16; ++w) {
+                for (uint32_t w = 0; w < 16; ++w) {
 #pragma unroll
-                for (uint32_t k = 0; k < 4; ++k) {
-                    const uint32_t idx = off + 4u * w + k;
-                    if (idx < n) {
-                        const uint8_t x = in[idx];
-                        const uint8_t y = x ^ (uint8_t)(ks[w] >> (8u * k));
-                        out[idx] = y;
-                        ct_lds[idx] = OPEN ? x : y;
+                    for (uint32_t k = 0; k < 4; ++k) {
+                        const uint32_t idx = off + 4u * w + k;
+                        if (idx < n) {
+                            const uint8_t x = in[idx];
+                            const uint8_t y = x ^ (uint8_t)(ks[w] >> (8u * k));
+                            out[idx] = y;
+                            ct_lds[idx] = OPEN ? x : y;
+                        }
                     }
                 }
             }
         }
-    }
 
-    // ---- MAC stream framing in LDS: ad || le64(|ad|) || ct || le64(|ct|) ----
-    const uint32_t adlen = p.tls ? 13u : p.ad_len;
-    const uint32_t S = A - adlen - 8u;  // stream start, >= kZeroRegion
-    const MacGeom g = mac_geom(adlen, n);
-    if (tid < 64u) {
-        const u32x4 zero = {0u, 0u, 0u, 0u};
-        st16(lds + 16u * tid, zero);  // [0, 2048): virtual blocks read zeros
-        st16(lds + 1024u + 16u * tid, zero);
-        if (kZeroRegion + tid < S) lds[kZeroRegion + tid] = 0;
-        for (uint32_t i = tid; i < adlen + 8u; i += 64u) {
-            uint8_t v;
-            if (i < adlen)
-                v = p.tls ? tls_ad_byte(rk.seq, p.tls_hdr, n, i) : p.ads[(uint64_t)p.ad_stride * rec + i];
-            else
-                v = (uint8_t)((uint64_t)adlen >> (8u * (i - adlen)));
-            lds[S + i] = v;
+        // ---- MAC stream framing: ad || le64(|ad|) || ct || le64(|ct|) --------
+        if (t < PL) {
+            const u32x4 zero = {0u, 0u, 0u, 0u};
+            st16(lds + 16u * t, zero);  // [0, Z): virtual blocks read zeros
+            st16(lds + 16u * (t + PL), zero);
+            if (Z + t < S) lds[Z + t] = 0;
+            for (uint32_t i = t; i < adlen + 8u; i += PL) {
+                uint8_t v;
+                if (i < adlen)
+                    v = p.tls ? tls_ad_byte(rk.seq, p.tls_hdr, n, i) : p.ads[(uint64_t)p.ad_stride * rec + i];
+                else
+                    v = (uint8_t)((uint64_t)adlen >> (8u * (i - adlen)));
+                lds[S + i] = v;
+            }
+            // suffix le64(n), then zeros to the end of the last block (+4 funnel bytes)
+            for (uint32_t i = t; i < 28u; i += PL) ct_lds[n + i] = i < 8u ? (uint8_t)((uint64_t)n >> (8u * i)) : 0;
         }
-        // suffix le64(n), then zeros to the end of the last block (+4 funnel bytes)
-        if (tid < 8u) ct_lds[n + tid] = (uint8_t)((uint64_t)n >> (8u * tid));
-        else if (tid < 8u + 20u) ct_lds[n + tid] = 0;
     }
     __syncthreads();
-    if (tid >= 64u) return;
+    if (!work || t >= PL) return;
 
-    // ---- phase 2 (wave 0): Poly1305 ----------------------------------------
+    // ---- phase 2: Poly1305 on PL lanes -----------------------------------------
+    const MacGeom g = mac_geom(adlen, n, PL);
     const uint32_t* kr = p.ws + (uint64_t)rec * kKeyRecWords;
-    const uint32_t r0 = uniform(kr[kR32Off + 0]), r1 = uniform(kr[kR32Off + 1]);
-    const uint32_t r2 = uniform(kr[kR32Off + 2]), r3 = uniform(kr[kR32Off + 3]);
+    uint32_t r0 = kr[kR32Off + 0], r1 = kr[kR32Off + 1], r2 = kr[kR32Off + 2], r3 = kr[kR32Off + 3];
+    if constexpr (PL == 64u) {  // one record per wave: keep the key in SGPRs
+        r0 = uniform(r0); r1 = uniform(r1); r2 = uniform(r2); r3 = uniform(r3);
+    }
     const uint32_t s1 = r1 + (r1 >> 2), s2 = r2 + (r2 >> 2), s3 = r3 + (r3 >> 2);
 
     // lane t: virtual blocks [t*k, t*k + k); virtual block v is real iff v >= z
     const uint32_t sh = (S & 3u) * 8u;
-    const uint32_t v0 = tid * g.k;
+    const uint32_t v0 = t * g.k;
     uint32_t pos = S - 16u * g.z + 16u * v0;
     const uint32_t* l32 = reinterpret_cast<const uint32_t*>(lds);
     const uint32_t rem = g.L - 16u * (g.B - 1u);  // bytes in the final block, 1..16
@@ -493,9 +508,9 @@ __global__ __launch_bounds__(256) void sg_aead_kernel(const KParams p) {
         uint32_t m3 = __builtin_amdgcn_alignbit(a4, a3, sh);
         uint32_t pad = (v0 + j >= g.z) ? 1u : 0u;  // 2^128 for a full real block
         if (j + 1u == g.k && rem < 16u) {
-            // lane 63 holds the final, partial block: pad bit at 8 * rem
+            // the last lane holds the final, partial block: pad bit at 8 * rem
             // (poly1305.rs:216-225; the bytes after the stream are zero)
-            if (tid == 63u) {
+            if (t == PL - 1u) {
                 const uint32_t fb = 1u << (8u * (rem & 3u));
                 const uint32_t fw = rem >> 2;
                 m0 |= fw == 0u ? fb : 0u;
@@ -508,7 +523,7 @@ __global__ __launch_bounds__(256) void sg_aead_kernel(const KParams p) {
         horner_step(h, m0, m1, m2, m3, pad, r0, r1, r2, r3, s1, s2, s3);
         pos += 16u;
     }
-    // radix 2^32 -> 2^26 for the tree (h < 2^131)
+    // radix 2^32 -> 2^26 (h < 2^131)
     F26 f = words_to_f26(h.h0, h.h1, h.h2, h.h3, 0u);
     f.v4 += h.h4 << 24;
     {
@@ -516,19 +531,18 @@ __global__ __launch_bounds__(256) void sg_aead_kernel(const KParams p) {
         f.v4 &= M26;
         f.v0 += c * 5u;
     }
-    // combine lanes: total = sum_t h_t R^(63-t), R = r^k.  Lane t = 8a + b
-    // scales by R^(63-t) = hi[7-a] * lo[7-b] (keying record), then the 64
-    // scaled values are summed limb-wise with shuffles.
+    // combine lanes: total = sum_t h_t R^(PL-1-t), R = r^k; R^e = hi[e >> 3] * lo[e & 7]
     {
-        const F26 plo = load_f26(kr + kPowLoOff + 5u * (7u - (tid & 7u)));
-        const F26 phi = load_f26(kr + kPowHiOff + 5u * (7u - (tid >> 3)));
+        const uint32_t e = PL - 1u - t;
+        const F26 plo = load_f26(kr + kPowLoOff + 5u * (e & 7u));
+        const F26 phi = load_f26(kr + kPowHiOff + 5u * (e >> 3));
         const F26 P = mul_add(phi, plo.v0, plo.v1, plo.v2, plo.v3, plo.v4, f26_zero());
         f = carry_full(mul_add(f, P.v0, P.v1, P.v2, P.v3, P.v4, f26_zero()));
     }
-    // limbs < 2^26: 32 of them sum below 2^31, so carry once before the last level
+    // limbs < 2^26: PL/2 <= 32 of them sum below 2^31, so carry once before the last level
 #pragma unroll
-    for (int l = 0; l < 6; ++l) {
-        if (l == 5) {
+    for (uint32_t d = 1; d < PL; d <<= 1) {
+        if (2u * d == PL) {
             uint32_t c;
             c = f.v0 >> 26; f.v0 &= M26; f.v1 += c;
             c = f.v1 >> 26; f.v1 &= M26; f.v2 += c;
@@ -536,34 +550,129 @@ __global__ __launch_bounds__(256) void sg_aead_kernel(const KParams p) {
             c = f.v3 >> 26; f.v3 &= M26; f.v4 += c;
             c = f.v4 >> 26; f.v4 &= M26; f.v0 += c * 5u;
         }
-        const int d = 1 << l;
-        f.v0 += __shfl_xor(f.v0, d, 64);
-        f.v1 += __shfl_xor(f.v1, d, 64);
-        f.v2 += __shfl_xor(f.v2, d, 64);
-        f.v3 += __shfl_xor(f.v3, d, 64);
-        f.v4 += __shfl_xor(f.v4, d, 64);
+        f.v0 += __shfl_xor(f.v0, (int)d, 64);
+        f.v1 += __shfl_xor(f.v1, (int)d, 64);
+        f.v2 += __shfl_xor(f.v2, (int)d, 64);
+        f.v3 += __shfl_xor(f.v3, (int)d, 64);
+        f.v4 += __shfl_xor(f.v4, (int)d, 64);
     }
-    if (tid != 0) return;
+    if (t != 0) return;
     uint32_t s[4] = {kr[kSOff + 0], kr[kSOff + 1], kr[kSOff + 2], kr[kSOff + 3]};
-    uint32_t t[4];
-    tag_words(f, s, t);
+    uint32_t tw[4];
+    tag_words(f, s, tw);
 
     if constexpr (!OPEN) {
         uint8_t* tp = out + n;  // ct || tag (chacha20_poly1305.rs:55)
         if ((((uintptr_t)tp) & 3u) == 0u) {
             uint32_t* t32 = reinterpret_cast<uint32_t*>(tp);
-            t32[0] = t[0]; t32[1] = t[1]; t32[2] = t[2]; t32[3] = t[3];
+            t32[0] = tw[0]; t32[1] = tw[1]; t32[2] = tw[2]; t32[3] = tw[3];
         } else {
 #pragma unroll
-            for (int i = 0; i < 16; ++i) tp[i] = (uint8_t)(t[i >> 2] >> (8 * (i & 3)));
+            for (int i = 0; i < 16; ++i) tp[i] = (uint8_t)(tw[i >> 2] >> (8 * (i & 3)));
         }
     } else {
         // constant-time compare: diff |= a ^ b over all 16 bytes (:84-87)
         const uint8_t* ep = in + n;
         uint32_t diff = 0;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) diff |= (uint32_t)(ep[i] ^ (uint8_t)(t[i >> 2] >> (8 * (i & 3))));
+        for (int i = 0; i < 16; ++i) diff |= (uint32_t)(ep[i] ^ (uint8_t)(tw[i >> 2] >> (8 * (i & 3))));
         p.status[rec] = diff != 0u ? 1u : 0u;
+    }
+}
+
+// Record slot of this lane's group.  For L >= 64 a group is a whole wave (or
+// the workgroup), so the slot is made provably uniform: the record's key,
+// nonce and lengths then live in SGPRs and the uniform first-round
+// quarter-rounds are hoisted to scalar code.
+template <uint32_t L>
+__device__ __forceinline__ uint32_t group_of_thread() {
+    if constexpr (L == 256u) return 0u;
+    else if constexpr (L >= 64u) return __builtin_amdgcn_readfirstlane(threadIdx.x / L);
+    else return threadIdx.x / L;
+}
+
+// Direct launch: workgroup w serves records w*RPW .. w*RPW + RPW - 1.
+template <bool OPEN, uint32_t L>
+__global__ __launch_bounds__(256) void sg_aead_kernel(const KParams p) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    constexpr uint32_t RPW = 256u / L;
+    const uint32_t g = group_of_thread<L>(), t = threadIdx.x % L;
+    const uint32_t rec = blockIdx.x * RPW + g;
+    aead_record<OPEN, L>(p, rec, rec < p.count, lds + g * p.lds_rec_bytes, t);
+}
+
+// Bucketed launch: records listed by sg_classify_kernel for this size class;
+// a fixed grid walks the list (the class population is only known on device).
+template <bool OPEN, uint32_t L>
+__global__ __launch_bounds__(256) void sg_aead_list_kernel(const KParams p, const uint32_t* __restrict__ list,
+                                                           const uint32_t* __restrict__ list_count) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    constexpr uint32_t RPW = 256u / L;
+    const uint32_t g = group_of_thread<L>(), t = threadIdx.x % L;
+    const uint32_t cnt = *list_count;
+    for (uint32_t base = blockIdx.x * RPW; base < cnt; base += gridDim.x * RPW) {
+        const uint32_t slot = base + g;
+        const bool active = slot < cnt;
+        uint32_t rec = active ? list[slot] : 0u;
+        if constexpr (L >= 64u) rec = __builtin_amdgcn_readfirstlane(rec);
+        aead_record<OPEN, L>(p, rec, active, lds + g * p.lds_rec_bytes, t);
+        __syncthreads();  // LDS is reused by the next iteration
+    }
+}
+
+// Size-class bucketing.  A 1024-thread workgroup classifies 4096 records:
+// per-wave ballots, then one device atomic per class per workgroup (a single
+// counter word takes only ~88 atomics/us, so per-wave atomics cost ~0.5 ms
+// for 1M records).
+constexpr uint32_t kClassifyThreads = 1024;
+constexpr uint32_t kClassifyPerThread = 4;
+
+template <bool OPEN>
+__global__ __launch_bounds__(1024) void sg_classify_kernel(const KParams p, uint32_t* __restrict__ lists,
+                                                           uint32_t* __restrict__ counts) {
+    __shared__ uint32_t wave_cnt[kNumClasses][kClassifyThreads / 64];
+    __shared__ uint32_t wg_base[kNumClasses];
+    const uint32_t lane = __lane_id(), wave = threadIdx.x >> 6;
+    const uint32_t rec0 = blockIdx.x * (kClassifyThreads * kClassifyPerThread);
+    uint32_t cls[kClassifyPerThread];
+    uint32_t mine[kNumClasses] = {0u, 0u, 0u, 0u};  // this wave's records per class
+#pragma unroll
+    for (uint32_t i = 0; i < kClassifyPerThread; ++i) {
+        const uint32_t rec = rec0 + i * kClassifyThreads + threadIdx.x;
+        cls[i] = kNumClasses;
+        if (rec < p.count) {
+            const uint32_t len = record_len(p, rec);
+            const uint32_t n = OPEN ? (len >= 16u ? len - 16u : 0u) : len;
+            cls[i] = size_class(n);
+        }
+#pragma unroll
+        for (uint32_t c = 0; c < kNumClasses; ++c) mine[c] += (uint32_t)__popcll(__ballot(cls[i] == c));
+    }
+    if (lane == 0)
+        for (uint32_t c = 0; c < kNumClasses; ++c) wave_cnt[c][wave] = mine[c];
+    __syncthreads();
+    if (threadIdx.x < kNumClasses) {
+        uint32_t tot = 0;
+        for (uint32_t w = 0; w < kClassifyThreads / 64; ++w) {
+            const uint32_t x = wave_cnt[threadIdx.x][w];
+            wave_cnt[threadIdx.x][w] = tot;  // exclusive prefix over waves
+            tot += x;
+        }
+        wg_base[threadIdx.x] = tot ? atomicAdd(&counts[threadIdx.x], tot) : 0u;
+    }
+    __syncthreads();
+    uint32_t off[kNumClasses];
+#pragma unroll
+    for (uint32_t c = 0; c < kNumClasses; ++c) off[c] = wg_base[c] + wave_cnt[c][wave];
+#pragma unroll
+    for (uint32_t i = 0; i < kClassifyPerThread; ++i) {
+        const uint32_t rec = rec0 + i * kClassifyThreads + threadIdx.x;
+#pragma unroll
+        for (uint32_t c = 0; c < kNumClasses; ++c) {
+            const uint64_t mask = __ballot(cls[i] == c);
+            if (cls[i] == c) lists[(uint64_t)c * p.count + off[c] + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull))] = rec;
+            off[c] += (uint32_t)__popcll(mask);
+        }
     }
 }
 
@@ -623,8 +732,6 @@ __global__ __launch_bounds__(256) void sg_compare_kernel(const uint8_t* a, uint6
 
 }  // namespace
 
-uint32_t lds_ct_off(uint32_t adlen) { return kZeroRegion + ((adlen + 8u + 15u) & ~15u); }
-
 hipError_t launch_keying(const KParams& p, bool open, hipStream_t s) {
     const uint32_t grid = (p.count + kKeyingThreads - 1u) / kKeyingThreads;
     if (open)
@@ -634,14 +741,67 @@ hipError_t launch_keying(const KParams& p, bool open, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_seal(const KParams& p, uint32_t lds, hipStream_t s) {
-    hipLaunchKernelGGL(sg_aead_kernel<false>, dim3(p.count), dim3(kThreads), lds, s, p);
+template <bool OPEN, uint32_t L>
+hipError_t launch_direct(const KParams& p, hipStream_t s) {
+    constexpr uint32_t RPW = 256u / L;
+    const uint32_t grid = (p.count + RPW - 1u) / RPW;
+    hipLaunchKernelGGL((sg_aead_kernel<OPEN, L>), dim3(grid), dim3(kThreads), RPW * p.lds_rec_bytes, s, p);
     return hipGetLastError();
 }
 
-hipError_t launch_open(const KParams& p, uint32_t lds, hipStream_t s) {
-    hipLaunchKernelGGL(sg_aead_kernel<true>, dim3(p.count), dim3(kThreads), lds, s, p);
+template <bool OPEN, uint32_t L>
+hipError_t launch_list(const KParams& p, const uint32_t* list, const uint32_t* cnt, hipStream_t s) {
+    constexpr uint32_t RPW = 256u / L;
+    uint32_t grid = (p.count + RPW - 1u) / RPW;
+    const uint32_t cap = kListGridPerCU * 256u;
+    if (grid > cap) grid = cap;
+    hipLaunchKernelGGL((sg_aead_list_kernel<OPEN, L>), dim3(grid), dim3(kThreads), RPW * p.lds_rec_bytes, s, p,
+                       list, cnt);
     return hipGetLastError();
+}
+
+template <bool OPEN>
+hipError_t launch_aead_t(const KParams& p, uint32_t max_n, bool uniform, uint32_t* lists, uint32_t* counts,
+                         hipStream_t s) {
+    if (uniform) {  // every record in one class: direct launch
+        KParams q = p;
+        const uint32_t c = size_class(max_n);
+        q.lds_rec_bytes = lds_rec_bytes(c, q.ad_len, max_n);
+        switch (c) {
+            case 0: return launch_direct<OPEN, 16>(q, s);
+            case 1: return launch_direct<OPEN, 64>(q, s);
+            case 2: return launch_direct<OPEN, 128>(q, s);
+            default: return launch_direct<OPEN, 256>(q, s);
+        }
+    }
+    hipError_t e = hipMemsetAsync(counts, 0, 16, s);
+    if (e != hipSuccess) return e;
+    const uint32_t per_wg = kClassifyThreads * kClassifyPerThread;
+    hipLaunchKernelGGL(sg_classify_kernel<OPEN>, dim3((p.count + per_wg - 1u) / per_wg), dim3(kClassifyThreads), 0, s,
+                       p, lists, counts);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    // one launch per populated class, largest records first
+    static const uint32_t class_max[kNumClasses] = {kClass0Max, kClass1Max, kClass2Max, 0xffffffffu};
+    KParams q = p;
+    for (int c = (int)size_class(max_n); c >= 0; --c) {
+        const uint32_t cap = max_n < class_max[c] ? max_n : class_max[c];
+        q.lds_rec_bytes = lds_rec_bytes((uint32_t)c, q.ad_len, cap);
+        const uint32_t* list = lists + (uint64_t)c * p.count;
+        switch (c) {
+            case 0: e = launch_list<OPEN, 16>(q, list, counts + 0, s); break;
+            case 1: e = launch_list<OPEN, 64>(q, list, counts + 1, s); break;
+            case 2: e = launch_list<OPEN, 128>(q, list, counts + 2, s); break;
+            default: e = launch_list<OPEN, 256>(q, list, counts + 3, s); break;
+        }
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+hipError_t launch_aead(const KParams& p, bool open, uint32_t max_n, bool uniform, uint32_t* lists,
+                       uint32_t* counts, hipStream_t s) {
+    return open ? launch_aead_t<true>(p, max_n, uniform, lists, counts, s)
+                : launch_aead_t<false>(p, max_n, uniform, lists, counts, s);
 }
 
 hipError_t launch_fill(uint8_t* buf, uint64_t stride, uint32_t len, uint32_t count, uint64_t seed,
@@ -663,9 +823,9 @@ hipError_t launch_compare(const uint8_t* a, uint64_t sa, const uint8_t* b, uint6
 }
 
 const char* kernel_config() {
-    return "gfx950 sg_aead_kernel v2: 256 threads/record, lane=64B ChaCha block, "
-           "wave0 Poly1305 contiguous-chunk Horner radix-2^32 (clamped r) + per-lane r^(k(63-t)) scale + shuffle sum, "
-           "keying pre-pass";
+    return "gfx950 sg_aead_kernel v4: size classes (16/64/128/256 lanes per record, device bucketing), "
+           "lane=64B ChaCha block, Poly1305 contiguous-chunk Horner radix-2^32 (clamped r) on 16/64 lanes + "
+           "per-lane r^(k(PL-1-t)) scale + shuffle sum, keying pre-pass";
 }
 
 }  // namespace sg

@@ -145,7 +145,8 @@ def test_c1_subset_4096_x_16kib_bit_exact(gpu, oracle):
     assert host(back) == pt_h and host(st) == bytes(count)
 
 
-@pytest.mark.parametrize("n", [0, 1, 15, 16, 17, 63, 64, 65, 100, 255, 256, 1000, 4095, 16383, 16384, 18432])
+@pytest.mark.parametrize("n", [0, 1, 15, 16, 17, 63, 64, 65, 100, 255, 256, 1000, 1024, 1025, 4095, 4096, 4097,
+                               5000, 8192, 8193, 16383, 16384, 18432])
 def test_batch_lengths(gpu, oracle, n):
     count = 33
     pt, ct, back, st = tls_batch(count, n, seq0=0xFFFFFFF0)
@@ -272,3 +273,39 @@ def test_c1_scale_roundtrip_and_tag_fold(gpu, oracle):
     ref = np.frombuffer(ct_ref, dtype=np.uint8).reshape(count, n + 16)
     for i in list(range(0, count, 4099)) + [count // 2, count - 1]:
         assert np.array_equal(ct_h[i].cpu().numpy(), ref[i]), i
+
+
+def test_c2_zipf_sample_bit_exact(gpu, oracle):
+    """C2 shape: Zipf 64 B-16 KiB, 256 connection keys, seq = i / 256; mixed
+    sizes go through device bucketing into all three size classes."""
+    torch = torch_mod()
+    from suruga_amd import batch as B
+    from suruga_amd import workloads as W
+
+    count = 3000
+    lay = W.c2_layout(count)
+    classes = {(int(x) > 1024) + (int(x) > 4096) + (int(x) > 8192) for x in lay.lens}
+    assert classes == {0, 1, 2, 3}
+    rng = np.random.default_rng(5)
+    pt_h = rng.bytes(lay.pt_bytes)
+    t64 = lambda a: torch.from_numpy(a.view(np.int64)).to("cuda")
+    t32 = lambda a: torch.from_numpy(a.view(np.int32)).to("cuda")
+    keys = dev_bytes(lay.keys).view(-1, 32)
+    ct = torch.zeros(lay.ct_bytes, dtype=torch.uint8, device="cuda")
+    maxl = int(lay.lens.max())
+    common = dict(count=count, keys=keys, key_index=t32(lay.key_index), seq=t64(lay.seq))
+    B.seal(B.Batch(inp=dev_bytes(pt_h), out=ct, lens=t32(lay.lens), max_len=maxl, in_off=t64(lay.in_off),
+                   out_off=t64(lay.out_off), **common))
+    torch.cuda.synchronize()
+    ct_h = host(ct)
+    for i in range(count):
+        k = lay.keys[32 * lay.key_index[i]:32 * lay.key_index[i] + 32]
+        s, n, o, q = int(lay.seq[i]), int(lay.lens[i]), int(lay.in_off[i]), int(lay.out_off[i])
+        exp = oracle.seal(k, struct.pack(">Q", s), pt_h[o:o + n], oracle.tls_ad(s, n))
+        assert ct_h[q:q + n + 16] == exp, (i, n)
+    back = torch.zeros(lay.pt_bytes, dtype=torch.uint8, device="cuda")
+    st = torch.full((count,), 0xFF, dtype=torch.uint8, device="cuda")
+    B.open_(B.Batch(inp=ct, out=back, lens=t32(lay.lens + 16), max_len=maxl + 16, in_off=t64(lay.out_off),
+                    out_off=t64(lay.in_off), status=st, **common))
+    torch.cuda.synchronize()
+    assert host(st) == bytes(count) and host(back) == pt_h
