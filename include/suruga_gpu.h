@@ -158,6 +158,59 @@ size_t sg_workspace_size(uint32_t count);
 int sg_seal_batch(const sg_batch* b);
 int sg_open_batch(const sg_batch* b);
 
+/* ---- batched record layer over host memory ------------------------------
+ * The throughput form of TlsWriter / TlsReader (tls.rs:68-380): many records
+ * per call, pinned double-buffered host<->device staging inside the library,
+ * wire format exactly as the reference writes and parses it:
+ *   header = content_type || major || minor || be16(fragment length)
+ *   (tls.rs:126-130, 218-236) followed by the fragment (ct || tag).        */
+#define SG_RECORD_MAX_LEN      16384u              /* RECORD_MAX_LEN      tls.rs:32 */
+#define SG_ENC_RECORD_MAX_LEN  (16384u + 2048u)    /* ENC_RECORD_MAX_LEN  tls.rs:35 */
+#define SG_HEADER_LEN          5u
+/* record-layer error codes (TlsErrorKind, tls_result.rs:5-20) */
+#define SG_E_UNEXPECTED_MESSAGE 3  /* unknown content type (tls.rs:218-225)          */
+#define SG_E_RECORD_OVERFLOW    4  /* fragment > 2^14 + 2048 (tls.rs:232-234), or a
+                                      decrypted fragment > 2^14 (tls.rs:269-272,
+                                      where the reference panics)                  */
+
+/* Upper bound of the wire bytes sg_write_records produces for len bytes. */
+size_t sg_wire_bound(size_t len);
+
+/* TlsWriter::write_data (tls.rs:137-147) + write_record (:99-135) for a whole
+ * buffer: `data` is cut into ceil(len / 2^14) fragments (len == 0 writes no
+ * record, as the reference's chunks() loop yields none), record i is sealed with
+ * seq = seq0 + i (nonce be64(seq), AD be64(seq)||type||major||minor||be16(n)),
+ * and its wire image is appended to `wire`.  Host memory in and out.
+ * Returns the number of records written (the caller adds it to its
+ * write_count, tls.rs:132) or < 0; *wire_len = bytes written. */
+int64_t sg_write_records(sg_ctx* ctx, uint64_t seq0, uint8_t content_type, uint8_t ver_major,
+                         uint8_t ver_minor, const uint8_t* data, size_t len, uint8_t* wire,
+                         size_t wire_cap, size_t* wire_len);
+
+/* TlsReader::read_record (tls.rs:217-281) for every COMPLETE record at the
+ * start of `wire`: header checks in the reference's order (unknown type ->
+ * SG_E_UNEXPECTED_MESSAGE, length > 2^14+2048 -> SG_E_RECORD_OVERFLOW,
+ * length < 16 -> SG_E_SHORT), AD = be64(seq)||type||major||minor||be16(len-16)
+ * with seq = seq0 + i, open, and append the plaintext fragments to `out`.
+ * Processing stops at the first failing record; the records before it are
+ * delivered.  Per-record content types / plaintext lengths go to `types` /
+ * `frag_lens` (capacity max_records, either may be NULL). */
+typedef struct sg_read_result {
+    uint64_t records;    /* records opened successfully (the caller adds this to read_count) */
+    uint64_t consumed;   /* wire bytes of those records                                     */
+    uint64_t out_len;    /* plaintext bytes written to out                                  */
+    int32_t  error;      /* SG_OK, or the status of record number `records`                 */
+    uint32_t _pad;
+} sg_read_result;
+int sg_read_records(sg_ctx* ctx, uint64_t seq0, const uint8_t* wire, size_t wire_len, uint8_t* out,
+                    size_t out_cap, uint8_t* types, uint32_t* frag_lens, size_t max_records,
+                    sg_read_result* res);
+
+/* Time (ms) spent by the last sg_write_records / sg_read_records call of this
+ * thread in host->device copies, kernels and device->host copies (HIP events;
+ * summed over the pipelined chunks) and in host-side framing memcpy. */
+int sg_record_timing(double* h2d_ms, double* kernel_ms, double* d2h_ms, double* host_ms);
+
 /* ---- synthetic workload helpers (bench / tests) ------------------------ */
 /* Fills records on the device: byte i of record j =
  * byte (i mod 8) of splitmix64(seed ^ ((j0 + j) << 32) ^ (i / 8)).

@@ -32,6 +32,7 @@ EXPORTS = [
     "sg_workspace_size", "sg_seal_batch", "sg_open_batch",
     "sg_fill_records", "sg_compare_records",
     "sg_last_error", "sg_build_info", "sg_set_timing", "sg_timing_read",
+    "sg_wire_bound", "sg_write_records", "sg_read_records", "sg_record_timing",
 ]
 
 
@@ -68,6 +69,20 @@ class SgBatch(C.Structure):
         ("workspace", C.c_void_p),
         ("workspace_size", C.c_size_t),
     ]
+
+
+class SgReadResult(C.Structure):
+    """Mirror of ``struct sg_read_result``."""
+
+    _fields_ = [("records", C.c_uint64), ("consumed", C.c_uint64), ("out_len", C.c_uint64),
+                ("error", C.c_int32), ("_pad", C.c_uint32)]
+
+
+SG_E_UNEXPECTED_MESSAGE = 3
+SG_E_RECORD_OVERFLOW = 4
+SG_RECORD_MAX_LEN = 16384
+SG_ENC_RECORD_MAX_LEN = 16384 + 2048
+SG_HEADER_LEN = 5
 
 
 class NativeError(RuntimeError):
@@ -113,6 +128,16 @@ def _declare(lib: C.CDLL) -> None:
     d = C.POINTER(C.c_double)
     u = C.POINTER(C.c_uint32)
     lib.sg_timing_read.argtypes = [d, d, d, u, u, u]
+    lib.sg_wire_bound.restype = C.c_size_t
+    lib.sg_wire_bound.argtypes = [C.c_size_t]
+    lib.sg_write_records.restype = C.c_int64
+    lib.sg_write_records.argtypes = [C.c_void_p, C.c_uint64, C.c_uint8, C.c_uint8, C.c_uint8, C.c_void_p,
+                                     C.c_size_t, C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t)]
+    lib.sg_read_records.restype = C.c_int
+    lib.sg_read_records.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t,
+                                    C.c_void_p, C.c_void_p, C.c_size_t, C.POINTER(SgReadResult)]
+    lib.sg_record_timing.restype = C.c_int
+    lib.sg_record_timing.argtypes = [d, d, d, d]
 
 
 def load(path: Path | None = None) -> C.CDLL:

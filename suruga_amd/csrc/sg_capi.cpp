@@ -14,13 +14,16 @@
 #include <vector>
 
 #include "../../include/suruga_gpu.h"
+#include "sg_host.h"
 #include "sg_internal.h"
 
 namespace {
-
 thread_local std::string g_err;
+}  // namespace
 
-int fail(int code, const char* fmt, const char* detail = nullptr) {
+namespace sg {
+
+int fail(int code, const char* fmt, const char* detail) {
     char buf[512];
     std::snprintf(buf, sizeof buf, fmt, detail ? detail : "");
     g_err = buf;
@@ -34,11 +37,12 @@ int hip_fail(hipError_t e, const char* where) {
     return SG_E_HIP;
 }
 
-#define SG_HIP(call)                                           \
-    do {                                                       \
-        hipError_t e_ = (call);                                \
-        if (e_ != hipSuccess) return hip_fail(e_, #call);      \
-    } while (0)
+}  // namespace sg
+
+namespace {
+
+using sg::fail;
+using sg::hip_fail;
 
 struct DeviceState {
     bool init = false;
@@ -212,18 +216,8 @@ int run_batch(const sg_batch* b, bool open) {
 // ---------------------------------------------------------------------------
 // single-record contexts (Encryptor / Decryptor)
 // ---------------------------------------------------------------------------
-struct sg_ctx {
-    int device;
-    uint8_t* d_key;      // 32 B
-    uint8_t* d_nonce;    // 8 B
-    uint8_t* d_ad;       // SG_MAX_AD_LEN
-    uint8_t* d_in;       // SG_MAX_RECORD_LEN + 16
-    uint8_t* d_out;      // SG_MAX_RECORD_LEN + 16
-    uint8_t* d_status;   // 1
-    void* d_ws;
-    hipStream_t stream;
-    std::mutex mu;
-};
+using sg::fail;
+using sg::hip_fail;
 
 extern "C" {
 
@@ -276,6 +270,7 @@ void sg_ctx_free(sg_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    sg::record_staging_free(c->rec);
     (void)hipFree(c->d_key);
     (void)hipFree(c->d_nonce);
     (void)hipFree(c->d_ad);

@@ -1,0 +1,43 @@
+// sg_host.h -- private host-side declarations shared by the C-ABI translation
+// units (sg_capi.cpp, sg_record.cpp).  Not part of the public ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <mutex>
+
+#include "../../include/suruga_gpu.h"
+
+namespace sg {
+
+// thread-local last-error message (sg_last_error)
+int fail(int code, const char* fmt, const char* detail = nullptr);
+int hip_fail(hipError_t e, const char* where);
+
+struct RecordStaging;                   // sg_record.cpp
+void record_staging_free(RecordStaging* rs);
+
+}  // namespace sg
+
+#define SG_HIP(call)                                                \
+    do {                                                            \
+        hipError_t e_ = (call);                                     \
+        if (e_ != hipSuccess) return sg::hip_fail(e_, #call);       \
+    } while (0)
+
+// One context per direction (Aead::new_encryptor / new_decryptor): the key on
+// the device, staging for single records, and (lazily) the record-layer
+// pipeline of sg_write_records / sg_read_records.
+struct sg_ctx {
+    int device = 0;
+    uint8_t* d_key = nullptr;      // 32 B
+    uint8_t* d_nonce = nullptr;    // 8 B
+    uint8_t* d_ad = nullptr;       // SG_MAX_AD_LEN
+    uint8_t* d_in = nullptr;       // SG_MAX_RECORD_LEN + 16
+    uint8_t* d_out = nullptr;      // SG_MAX_RECORD_LEN + 16
+    uint8_t* d_status = nullptr;   // 1
+    void* d_ws = nullptr;
+    hipStream_t stream = nullptr;
+    sg::RecordStaging* rec = nullptr;
+    std::mutex mu;
+};

@@ -1,0 +1,378 @@
+// sg_record.cpp -- batched record layer over host memory (sg_write_records /
+// sg_read_records): the throughput form of suruga's TlsWriter::write_data and
+// TlsReader::read_record (src/tls.rs:99-147, 217-281).
+//
+// Records move through a per-context pipeline of two slots.  Each slot owns
+// pinned host buffers, device buffers, a stream and a keying workspace; while
+// the GPU seals/opens chunk c on one slot, the CPU frames chunk c-1's output
+// and stages chunk c+1 on the other.  Device layout is always 16-byte aligned
+// (record slot stride kSlot), so the kernels take their vector path; the
+// 5-byte TLS headers are added/stripped by the CPU while copying.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <vector>
+
+#include "../../include/suruga_gpu.h"
+#include "sg_host.h"
+#include "sg_internal.h"
+
+namespace sg {
+
+namespace {
+constexpr uint32_t kChunk = 256;                                  // records per pipeline chunk
+constexpr uint32_t kSlot = ((SG_ENC_RECORD_MAX_LEN + 63u) / 64u) * 64u;  // device bytes per record
+constexpr uint32_t kMetaBytes = 8u + 13u;                         // nonce + AD per record (reader)
+
+thread_local double t_h2d = 0, t_kernel = 0, t_d2h = 0, t_host = 0;
+
+double now_ms() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+}  // namespace
+
+struct RecordStaging {
+    struct Slot {
+        uint8_t *h_in = nullptr, *h_out = nullptr, *h_meta = nullptr, *h_status = nullptr;
+        uint32_t* h_len = nullptr;
+        uint8_t *d_in = nullptr, *d_out = nullptr, *d_meta = nullptr, *d_status = nullptr;
+        uint32_t* d_len = nullptr;
+        void* d_ws = nullptr;
+        hipStream_t st = nullptr;
+        hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};  // start, after H2D, after kernels, after D2H
+        uint32_t nrec = 0;       // records in flight on this slot
+        uint64_t first = 0;      // index of its first record in the call
+        bool busy = false;
+    } slot[2];
+};
+
+void record_staging_free(RecordStaging* rs) {
+    if (!rs) return;
+    for (auto& s : rs->slot) {
+        if (s.st) (void)hipStreamSynchronize(s.st);
+        (void)hipHostFree(s.h_in);
+        (void)hipHostFree(s.h_out);
+        (void)hipHostFree(s.h_meta);
+        (void)hipHostFree(s.h_status);
+        (void)hipHostFree(s.h_len);
+        (void)hipFree(s.d_in);
+        (void)hipFree(s.d_out);
+        (void)hipFree(s.d_meta);
+        (void)hipFree(s.d_status);
+        (void)hipFree(s.d_len);
+        (void)hipFree(s.d_ws);
+        for (auto& e : s.ev)
+            if (e) (void)hipEventDestroy(e);
+        if (s.st) (void)hipStreamDestroy(s.st);
+    }
+    delete rs;
+}
+
+namespace {
+
+int staging(sg_ctx* c, RecordStaging** out) {
+    if (!c->rec) {
+        auto* rs = new RecordStaging();
+        c->rec = rs;  // freed with the context even if allocation below fails
+        const size_t bytes = (size_t)kChunk * kSlot;
+        for (auto& s : rs->slot) {
+            SG_HIP(hipHostMalloc((void**)&s.h_in, bytes, hipHostMallocDefault));
+            SG_HIP(hipHostMalloc((void**)&s.h_out, bytes, hipHostMallocDefault));
+            SG_HIP(hipHostMalloc((void**)&s.h_meta, (size_t)kChunk * kMetaBytes, hipHostMallocDefault));
+            SG_HIP(hipHostMalloc((void**)&s.h_status, kChunk, hipHostMallocDefault));
+            SG_HIP(hipHostMalloc((void**)&s.h_len, kChunk * 4u, hipHostMallocDefault));
+            SG_HIP(hipMalloc((void**)&s.d_in, bytes));
+            SG_HIP(hipMalloc((void**)&s.d_out, bytes));
+            SG_HIP(hipMalloc((void**)&s.d_meta, (size_t)kChunk * kMetaBytes));
+            SG_HIP(hipMalloc((void**)&s.d_status, kChunk));
+            SG_HIP(hipMalloc((void**)&s.d_len, kChunk * 4u));
+            SG_HIP(hipMalloc(&s.d_ws, sg_workspace_size(kChunk)));
+            SG_HIP(hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking));
+            for (auto& e : s.ev) SG_HIP(hipEventCreate(&e));
+        }
+    }
+    *out = c->rec;
+    return SG_OK;
+}
+
+// Wait for a slot's work and account its device times.
+int drain(RecordStaging::Slot& s) {
+    SG_HIP(hipEventSynchronize(s.ev[3]));
+    float a = 0, b = 0, d = 0;
+    SG_HIP(hipEventElapsedTime(&a, s.ev[0], s.ev[1]));
+    SG_HIP(hipEventElapsedTime(&b, s.ev[1], s.ev[2]));
+    SG_HIP(hipEventElapsedTime(&d, s.ev[2], s.ev[3]));
+    t_h2d += a;
+    t_kernel += b;
+    t_d2h += d;
+    s.busy = false;
+    return SG_OK;
+}
+
+inline void put_be16(uint8_t* p, uint32_t v) {
+    p[0] = (uint8_t)(v >> 8);
+    p[1] = (uint8_t)v;
+}
+inline void put_be64(uint8_t* p, uint64_t v) {
+    for (int i = 0; i < 8; ++i) p[i] = (uint8_t)(v >> (56 - 8 * i));
+}
+
+}  // namespace
+}  // namespace sg
+
+using sg::fail;
+
+extern "C" {
+
+size_t sg_wire_bound(size_t len) {
+    const size_t recs = (len + SG_RECORD_MAX_LEN - 1) / SG_RECORD_MAX_LEN;
+    return len + recs * (SG_HEADER_LEN + SG_MAC_LEN);
+}
+
+int sg_record_timing(double* h2d_ms, double* kernel_ms, double* d2h_ms, double* host_ms) {
+    if (h2d_ms) *h2d_ms = sg::t_h2d;
+    if (kernel_ms) *kernel_ms = sg::t_kernel;
+    if (d2h_ms) *d2h_ms = sg::t_d2h;
+    if (host_ms) *host_ms = sg::t_host;
+    return SG_OK;
+}
+
+int64_t sg_write_records(sg_ctx* c, uint64_t seq0, uint8_t content_type, uint8_t ver_major, uint8_t ver_minor,
+                         const uint8_t* data, size_t len, uint8_t* wire, size_t wire_cap, size_t* wire_len) {
+    using namespace sg;
+    if (!c || (!data && len) || !wire_len) return fail(SG_E_ARG, "NULL argument%s");
+    *wire_len = 0;
+    t_h2d = t_kernel = t_d2h = t_host = 0;
+    const uint64_t nrec = (len + SG_RECORD_MAX_LEN - 1) / SG_RECORD_MAX_LEN;
+    if (nrec == 0) return 0;
+    if (!wire || wire_cap < sg_wire_bound(len)) return fail(SG_E_ARG, "wire buffer too small%s");
+    std::lock_guard<std::mutex> lk(c->mu);
+    SG_HIP(hipSetDevice(c->device));
+    RecordStaging* rs = nullptr;
+    int rc = staging(c, &rs);
+    if (rc != SG_OK) return rc;
+    size_t wpos = 0;
+
+    // frame a drained slot's records into the wire (tls.rs:126-130)
+    auto emit = [&](RecordStaging::Slot& s) {
+        const double t0 = now_ms();
+        for (uint32_t i = 0; i < s.nrec; ++i) {
+            const uint64_t r = s.first + i;
+            const uint32_t n = (uint32_t)std::min<uint64_t>(SG_RECORD_MAX_LEN, len - r * SG_RECORD_MAX_LEN);
+            uint8_t* h = wire + wpos;
+            h[0] = content_type;
+            h[1] = ver_major;
+            h[2] = ver_minor;
+            put_be16(h + 3, n + SG_MAC_LEN);
+            std::memcpy(h + SG_HEADER_LEN, s.h_out + (size_t)i * kSlot, n + SG_MAC_LEN);
+            wpos += SG_HEADER_LEN + n + SG_MAC_LEN;
+        }
+        t_host += now_ms() - t0;
+    };
+
+    uint64_t next = 0;
+    int cur = 0;
+    while (next < nrec || rs->slot[0].busy || rs->slot[1].busy) {
+        RecordStaging::Slot& s = rs->slot[cur];
+        if (s.busy) {  // oldest chunk first: keeps the wire in record order
+            if ((rc = drain(s)) != SG_OK) return rc;
+            emit(s);
+        }
+        if (next < nrec) {
+            const uint32_t k = (uint32_t)std::min<uint64_t>(kChunk, nrec - next);
+            const double t0 = now_ms();
+            for (uint32_t i = 0; i < k; ++i) {
+                const uint64_t r = next + i;
+                const uint32_t n = (uint32_t)std::min<uint64_t>(SG_RECORD_MAX_LEN, len - r * SG_RECORD_MAX_LEN);
+                std::memcpy(s.h_in + (size_t)i * kSlot, data + r * SG_RECORD_MAX_LEN, n);
+                s.h_len[i] = n;
+            }
+            t_host += now_ms() - t0;
+            SG_HIP(hipEventRecord(s.ev[0], s.st));
+            SG_HIP(hipMemcpyAsync(s.d_in, s.h_in, (size_t)k * kSlot, hipMemcpyHostToDevice, s.st));
+            SG_HIP(hipMemcpyAsync(s.d_len, s.h_len, k * 4u, hipMemcpyHostToDevice, s.st));
+            SG_HIP(hipEventRecord(s.ev[1], s.st));
+            sg_batch b;
+            std::memset(&b, 0, sizeof b);
+            b.count = k;
+            b.flags = SG_BATCH_TLS;
+            b.keys = c->d_key;
+            b.num_keys = 1;
+            b.seq0 = seq0 + next;
+            b.content_type = content_type;
+            b.ver_major = ver_major;
+            b.ver_minor = ver_minor;
+            b.in = s.d_in;
+            b.in_stride = kSlot;
+            b.out = s.d_out;
+            b.out_stride = kSlot;
+            b.len = s.d_len;
+            b.max_len = SG_RECORD_MAX_LEN;
+            b.stream = s.st;
+            b.workspace = s.d_ws;
+            b.workspace_size = sg_workspace_size(kChunk);
+            if ((rc = sg_seal_batch(&b)) != SG_OK) return rc;
+            SG_HIP(hipEventRecord(s.ev[2], s.st));
+            SG_HIP(hipMemcpyAsync(s.h_out, s.d_out, (size_t)k * kSlot, hipMemcpyDeviceToHost, s.st));
+            SG_HIP(hipEventRecord(s.ev[3], s.st));
+            s.nrec = k;
+            s.first = next;
+            s.busy = true;
+            next += k;
+        }
+        cur ^= 1;
+    }
+    *wire_len = wpos;
+    return (int64_t)nrec;
+}
+
+int sg_read_records(sg_ctx* c, uint64_t seq0, const uint8_t* wire, size_t wire_len, uint8_t* out, size_t out_cap,
+                    uint8_t* types, uint32_t* frag_lens, size_t max_records, sg_read_result* res) {
+    using namespace sg;
+    if (!c || (!wire && wire_len) || !res) return fail(SG_E_ARG, "NULL argument%s");
+    std::memset(res, 0, sizeof *res);
+    t_h2d = t_kernel = t_d2h = t_host = 0;
+
+    // 1. parse complete records (tls.rs:218-238), stopping at the first bad header
+    struct Rec {
+        size_t off;      // wire offset of the fragment
+        uint32_t flen;   // fragment length (ct || tag)
+        uint8_t type, major, minor;
+    };
+    std::vector<Rec> recs;
+    size_t pos = 0;
+    int32_t header_error = SG_OK;
+    while (pos + SG_HEADER_LEN <= wire_len && recs.size() < max_records) {
+        const uint8_t* h = wire + pos;
+        if (h[0] < 20 || h[0] > 23) {  // ContentType 20..23 (tls.rs:19-29, 218-225)
+            header_error = SG_E_UNEXPECTED_MESSAGE;
+            break;
+        }
+        const uint32_t flen = ((uint32_t)h[3] << 8) | h[4];
+        if (flen > SG_ENC_RECORD_MAX_LEN) {  // tls.rs:232-234
+            header_error = SG_E_RECORD_OVERFLOW;
+            break;
+        }
+        if (pos + SG_HEADER_LEN + flen > wire_len) break;  // incomplete: wait for more bytes
+        if (flen < SG_MAC_LEN) {  // tls.rs:258-262 "encrypted message too short"
+            header_error = SG_E_SHORT;
+            break;
+        }
+        if (flen - SG_MAC_LEN > SG_RECORD_MAX_LEN) {  // tls.rs:269-272 (reference panics)
+            header_error = SG_E_RECORD_OVERFLOW;
+            break;
+        }
+        recs.push_back({pos + SG_HEADER_LEN, flen, h[0], h[1], h[2]});
+        pos += SG_HEADER_LEN + flen;
+    }
+    size_t need = 0;
+    for (const Rec& r : recs) need += r.flen - SG_MAC_LEN;
+    if (need > out_cap || (need && !out)) return fail(SG_E_ARG, "out buffer too small%s");
+    if (recs.empty()) {
+        res->error = header_error;
+        return SG_OK;
+    }
+
+    std::lock_guard<std::mutex> lk(c->mu);
+    SG_HIP(hipSetDevice(c->device));
+    RecordStaging* rs = nullptr;
+    int rc = staging(c, &rs);
+    if (rc != SG_OK) return rc;
+
+    const uint64_t nrec = recs.size();
+    uint64_t next = 0, good = 0, opos = 0, consumed = 0;
+    int32_t error = SG_OK;
+    auto collect = [&](RecordStaging::Slot& s) {
+        const double t0 = now_ms();
+        for (uint32_t i = 0; i < s.nrec && error == SG_OK; ++i) {
+            const uint64_t r = s.first + i;
+            const Rec& R = recs[r];
+            if (s.h_status[i] != 0) {  // BadRecordMac "wrong mac": deliver nothing of it
+                error = s.h_status[i] == 2 ? SG_E_SHORT : SG_E_BAD_MAC;
+                break;
+            }
+            const uint32_t n = R.flen - SG_MAC_LEN;
+            std::memcpy(out + opos, s.h_out + (size_t)i * kSlot, n);
+            if (types) types[r] = R.type;
+            if (frag_lens) frag_lens[r] = n;
+            opos += n;
+            consumed += SG_HEADER_LEN + R.flen;
+            ++good;
+        }
+        t_host += now_ms() - t0;
+    };
+
+    int cur = 0;
+    while (next < nrec || rs->slot[0].busy || rs->slot[1].busy) {
+        RecordStaging::Slot& s = rs->slot[cur];
+        if (s.busy) {
+            if ((rc = drain(s)) != SG_OK) return rc;
+            collect(s);
+        }
+        if (next < nrec && error == SG_OK) {
+            const uint32_t k = (uint32_t)std::min<uint64_t>(kChunk, nrec - next);
+            const double t0 = now_ms();
+            for (uint32_t i = 0; i < k; ++i) {
+                const Rec& R = recs[next + i];
+                const uint64_t seq = seq0 + next + i;
+                std::memcpy(s.h_in + (size_t)i * kSlot, wire + R.off, R.flen);
+                s.h_len[i] = R.flen;
+                // nonce = be64(seq) (tls.rs:250); AD = seq || type || major || minor ||
+                // be16(len - 16) (tls.rs:252-265).  Layout: nonces[kChunk][8], ads[kChunk][13]
+                put_be64(s.h_meta + 8u * i, seq);
+                uint8_t* m = s.h_meta + 8u * kChunk + 13u * i;
+                put_be64(m, seq);
+                m[8] = R.type;
+                m[9] = R.major;
+                m[10] = R.minor;
+                put_be16(m + 11, R.flen - SG_MAC_LEN);
+            }
+            t_host += now_ms() - t0;
+            SG_HIP(hipEventRecord(s.ev[0], s.st));
+            SG_HIP(hipMemcpyAsync(s.d_in, s.h_in, (size_t)k * kSlot, hipMemcpyHostToDevice, s.st));
+            SG_HIP(hipMemcpyAsync(s.d_len, s.h_len, k * 4u, hipMemcpyHostToDevice, s.st));
+            SG_HIP(hipMemcpyAsync(s.d_meta, s.h_meta, 8u * k, hipMemcpyHostToDevice, s.st));
+            SG_HIP(hipMemcpyAsync(s.d_meta + 8u * kChunk, s.h_meta + 8u * kChunk, 13u * k, hipMemcpyHostToDevice,
+                                  s.st));
+            SG_HIP(hipEventRecord(s.ev[1], s.st));
+            sg_batch b;
+            std::memset(&b, 0, sizeof b);
+            b.count = k;
+            b.keys = c->d_key;
+            b.num_keys = 1;
+            b.nonces = s.d_meta;
+            b.ads = s.d_meta + 8u * kChunk;
+            b.ad_len = 13;
+            b.ad_stride = 13;
+            b.in = s.d_in;
+            b.in_stride = kSlot;
+            b.out = s.d_out;
+            b.out_stride = kSlot;
+            b.len = s.d_len;
+            b.max_len = SG_ENC_RECORD_MAX_LEN;
+            b.status = s.d_status;
+            b.stream = s.st;
+            b.workspace = s.d_ws;
+            b.workspace_size = sg_workspace_size(kChunk);
+            if ((rc = sg_open_batch(&b)) != SG_OK) return rc;
+            SG_HIP(hipEventRecord(s.ev[2], s.st));
+            SG_HIP(hipMemcpyAsync(s.h_out, s.d_out, (size_t)k * kSlot, hipMemcpyDeviceToHost, s.st));
+            SG_HIP(hipMemcpyAsync(s.h_status, s.d_status, k, hipMemcpyDeviceToHost, s.st));
+            SG_HIP(hipEventRecord(s.ev[3], s.st));
+            s.nrec = k;
+            s.first = next;
+            s.busy = true;
+            next += k;
+        }
+        cur ^= 1;
+    }
+    res->records = good;
+    res->consumed = consumed;
+    res->out_len = opos;
+    res->error = error != SG_OK ? error : (good == nrec ? header_error : SG_OK);
+    return SG_OK;
+}
+
+}  // extern "C"

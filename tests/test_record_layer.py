@@ -1,0 +1,243 @@
+"""Record layer (src/tls.rs, src/test.rs): the reference's own record tests
+with the null cipher (CPU), and the batched GPU write/read paths checked
+against the oracle-backed per-record path (GPU)."""
+from __future__ import annotations
+
+import io
+import struct
+
+import pytest
+
+from suruga_amd.cipher import Decryptor, Encryptor, TlsError, TlsErrorKind
+from suruga_amd.tls import (ENC_RECORD_MAX_LEN, RECORD_MAX_LEN, ContentType, Record, RecordStreamReader,
+                            TlsReader, TlsWriter)
+
+
+class NullEncryptor(Encryptor):  # src/test.rs:13-20
+    def encrypt(self, nonce, plain, ad):
+        return bytes(plain)
+
+
+class NullDecryptor(Decryptor):  # src/test.rs:22-27
+    def decrypt(self, nonce, encrypted, ad):
+        return bytes(encrypted)
+
+    def mac_len(self):
+        return 0
+
+
+class OracleEncryptor(Encryptor):
+    """The CPU restatement behind the Encryptor trait (test infrastructure)."""
+
+    def __init__(self, oracle, key):
+        self.o, self.key = oracle, key
+
+    def encrypt(self, nonce, plain, ad):
+        return self.o.seal(self.key, nonce, plain, ad)
+
+
+class OracleDecryptor(Decryptor):
+    def __init__(self, oracle, key):
+        self.o, self.key = oracle, key
+
+    def decrypt(self, nonce, encrypted, ad):
+        rc, pt = self.o.open(self.key, nonce, encrypted, ad)
+        if rc == 2:
+            raise TlsError(TlsErrorKind.BadRecordMac, "message too short")
+        if rc != 0:
+            raise TlsError(TlsErrorKind.BadRecordMac, "wrong mac")
+        return pt
+
+    def mac_len(self):
+        return 16
+
+
+def null_tls(reader, writer):  # src/test.rs:29-39
+    r, w = TlsReader(reader), TlsWriter(writer)
+    r.set_decryptor(NullDecryptor())
+    w.set_encryptor(NullEncryptor())
+    return r, w
+
+
+# ---- src/test.rs ------------------------------------------------------------
+def test_change_cipher_spec_message():
+    out = io.BytesIO()
+    _, w = null_tls(io.BytesIO(), out)
+    w.write_change_cipher_spec()
+    data = out.getvalue()
+    assert len(data) == 1 + 2 + 2 + 1 and data[5] == 1
+    r, _ = null_tls(io.BytesIO(data), io.BytesIO())
+    assert r.read_message() == ("ChangeCipherSpec", None)
+
+
+def test_application_message():
+    app = b"\x01" * (RECORD_MAX_LEN + 200)
+    out = io.BytesIO()
+    _, w = null_tls(io.BytesIO(), out)
+    w.write_application_data(app)
+    r, _ = null_tls(io.BytesIO(out.getvalue()), io.BytesIO())
+    assert r.read_message() == ("ApplicationData", b"\x01" * RECORD_MAX_LEN)
+    assert r.read_message() == ("ApplicationData", b"\x01" * 200)
+
+
+# ---- src/tls.rs:382-476 ----------------------------------------------------------
+def test_reader():
+    r = TlsReader(io.BytesIO(bytes([0x14, 0x03, 0x03, 0x00, 0x01, 0x01])))
+    rec = r.read_record()
+    assert (rec.content_type, rec.ver_major, rec.ver_minor, rec.fragment) == \
+        (ContentType.ChangeCipherSpecTy, 3, 3, b"\x01")
+    with pytest.raises(TlsError) as e:
+        r.read_record()
+    assert e.value.kind is TlsErrorKind.IoFailure
+
+
+def test_reader_unknown():
+    r = TlsReader(io.BytesIO(bytes([0x18, 0x03, 0x03, 0x00, 0x03, 0x01, 0x00, 0x20])))
+    with pytest.raises(TlsError) as e:
+        r.read_record()
+    assert e.value.kind is TlsErrorKind.UnexpectedMessage
+
+
+def test_reader_too_long():
+    n = RECORD_MAX_LEN + 1
+    r = TlsReader(io.BytesIO(bytes([0x17, 0x03, 0x03, n >> 8, n & 0xFF]) + b"\xff" * n))
+    with pytest.raises(TlsError) as e:
+        r.read_record()
+    assert e.value.kind is TlsErrorKind.RecordOverflow
+
+
+def test_reader_zero_length():
+    for ct in (20, 21, 22):
+        r = TlsReader(io.BytesIO(bytes([ct, 0x03, 0x03, 0x00, 0x00])))
+        with pytest.raises(TlsError) as e:
+            r.read_message()
+        assert e.value.kind is TlsErrorKind.UnexpectedMessage
+
+
+def test_writer_too_long():
+    class Enc(Encryptor):
+        def encrypt(self, nonce, fragment, ad):
+            return bytes(ENC_RECORD_MAX_LEN + 1)
+
+    w = TlsWriter(io.BytesIO())
+    w.set_encryptor(Enc())
+    with pytest.raises(AssertionError):
+        w.write_record(Record(ContentType.ApplicationDataTy, 3, 3, b"\x01"))
+
+
+def test_record_framing_with_oracle_cipher(oracle):
+    """write_record framing + AD/nonce rules through the reference algorithm."""
+    key = bytes(range(32))
+    out = io.BytesIO()
+    w = TlsWriter(out)
+    w.set_encryptor(OracleEncryptor(oracle, key))
+    w.write_application_data(b"A" * 16)
+    wire = out.getvalue()
+    assert wire[:5] == bytes([23, 3, 3, 0, 32])
+    # the survey's sample vector: seq 0, type 23, ver 3.3
+    assert wire[5:].hex() == "59f90370eca7e79052201d20ee020f66fbc2d9037460b094b3443d3ec89ef135"
+    r = TlsReader(io.BytesIO(wire))
+    r.set_decryptor(OracleDecryptor(oracle, key))
+    assert r.read_application_data() == b"A" * 16
+
+
+# ---- GPU: batched record layer -------------------------------------------------
+@pytest.mark.gpu
+def test_gpu_batched_writer_matches_reference_reader(gpu, oracle):
+    from suruga_amd import ChaCha20Poly1305
+
+    key = bytes(range(32))
+    data = oracle.fill_record(0x53555255, 1, 5 * RECORD_MAX_LEN + 1234)
+    out = io.BytesIO()
+    w = TlsWriter(out)
+    w.set_encryptor(ChaCha20Poly1305().new_encryptor(key))
+    w.write_change_cipher_spec()          # 1 record (seq 0), batched path
+    w.write_application_data(data)        # 6 records (seq 1..6)
+    w.write_application_data(b"tail")     # seq 7
+    assert w.write_count == 8
+    r = TlsReader(io.BytesIO(out.getvalue()))
+    r.set_decryptor(OracleDecryptor(oracle, key))
+    assert r.read_message() == ("ChangeCipherSpec", None)
+    got = b"".join(r.read_application_data() for _ in range(6))
+    assert got == data and r.read_application_data() == b"tail"
+
+
+@pytest.mark.gpu
+def test_gpu_stream_reader_matches_reference_writer(gpu, oracle):
+    from suruga_amd import ChaCha20Poly1305
+
+    key = bytes(range(1, 33))
+    out = io.BytesIO()
+    w = TlsWriter(out)
+    w.set_encryptor(OracleEncryptor(oracle, key))
+    pieces = [oracle.fill_record(7, j, n) for j, n in enumerate([0, 1, 100, RECORD_MAX_LEN, 3000, 17])]
+    for p in pieces:
+        w.write_application_data(p)  # write of 0 bytes emits no record
+    wire = out.getvalue()
+    rd = RecordStreamReader(None, ChaCha20Poly1305().new_decryptor(key))
+    # feed in uneven slices: partial records stay buffered
+    got = []
+    for i in range(0, len(wire), 7777):
+        rd.feed(wire[i:i + 7777])
+        got += rd.drain()
+    assert [p for _, p in got] == [p for p in pieces if p]
+    assert all(t is ContentType.ApplicationDataTy for t, _ in got)
+    assert rd.read_count == 5 and not rd.buf
+
+
+@pytest.mark.gpu
+def test_gpu_stream_reader_errors(gpu, oracle):
+    from suruga_amd import ChaCha20Poly1305
+
+    key = bytes(32)
+    out = io.BytesIO()
+    w = TlsWriter(out)
+    w.set_encryptor(OracleEncryptor(oracle, key))
+    for j in range(4):
+        w.write_application_data(bytes([j]) * 500)
+    wire = bytearray(out.getvalue())
+    rec = 5 + 516
+    wire[2 * rec + 10] ^= 0x40  # corrupt record 2
+    rd = RecordStreamReader(None, ChaCha20Poly1305().new_decryptor(key))
+    rd.feed(bytes(wire))
+    with pytest.raises(TlsError) as e:
+        rd.drain()
+    assert e.value.kind is TlsErrorKind.BadRecordMac
+    assert rd.read_count == 2 and len(rd.buf) == 2 * rec  # records 0, 1 delivered
+    # unknown content type after a good record
+    rd2 = RecordStreamReader(None, ChaCha20Poly1305().new_decryptor(key))
+    rd2.feed(bytes(out.getvalue()[:rec]) + bytes([0x18, 3, 3, 0, 3, 1, 2, 3]))
+    with pytest.raises(TlsError) as e:
+        rd2.drain()
+    assert e.value.kind is TlsErrorKind.UnexpectedMessage and rd2.read_count == 1
+    # oversize header
+    rd3 = RecordStreamReader(None, ChaCha20Poly1305().new_decryptor(key))
+    n = ENC_RECORD_MAX_LEN + 1
+    rd3.feed(bytes([23, 3, 3, n >> 8, n & 0xFF]))
+    with pytest.raises(TlsError) as e:
+        rd3.drain()
+    assert e.value.kind is TlsErrorKind.RecordOverflow
+
+
+@pytest.mark.gpu
+def test_gpu_per_record_reader(gpu, oracle):
+    """The trait-object path: TlsReader.read_record -> Decryptor.decrypt on the GPU."""
+    from suruga_amd import ChaCha20Poly1305
+
+    key = bytes(range(32))
+    out = io.BytesIO()
+    w = TlsWriter(out)
+    w.set_encryptor(OracleEncryptor(oracle, key))
+    w.write_application_data(b"x" * 40000)
+    r = TlsReader(io.BytesIO(out.getvalue()))
+    r.set_decryptor(ChaCha20Poly1305().new_decryptor(key))
+    assert b"".join(r.read_application_data() for _ in range(3)) == b"x" * 40000
+    tampered = bytearray(out.getvalue())
+    tampered[-1] ^= 1
+    r = TlsReader(io.BytesIO(bytes(tampered)))
+    r.set_decryptor(ChaCha20Poly1305().new_decryptor(key))
+    r.read_record(), r.read_record()
+    with pytest.raises(TlsError) as e:
+        r.read_record()
+    assert e.value.kind is TlsErrorKind.BadRecordMac
+    assert struct.pack(">Q", r.read_count) == bytes(7) + b"\x02"

@@ -1,0 +1,155 @@
+#!/usr/bin/env python3
+"""C4 of BASELINE.json: an application stream through the GPU record layer
+over a loopback TCP connection, host<->device copies included.
+
+Writer thread: TlsWriter-style batched sealing (sg_write_records: fragment into
+2^14-byte records, seal on the GPU with pinned double-buffered staging, frame
+5-byte headers) and socket.sendall.  Reader thread: recv into a buffer and
+sg_read_records (parse headers, open on the GPU, strip framing).  Keys are
+fixed (the handshake is bypassed, as in src/test.rs:29-39's null_tls); every
+received byte is compared with what was sent.
+
+Prints one JSON line: end-to-end GiB/s of application data plus the time each
+side spent in H2D copies, kernels, D2H copies, host framing and socket I/O.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import socket
+import sys
+import threading
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+
+from suruga_amd import ChaCha20Poly1305  # noqa: E402
+from suruga_amd import _native as N  # noqa: E402
+
+KEY_C2S = bytes(range(32))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--bytes", type=int, default=1 << 30, help="application bytes (C4: 1 GiB)")
+    ap.add_argument("--write-chunk", type=int, default=16 << 20, help="bytes per write_application_data call")
+    ap.add_argument("--device", type=int, default=0)
+    args = ap.parse_args()
+    lib = N.load()
+    total, wchunk = args.bytes, args.write_chunk
+    pattern = np.random.default_rng(0xC4).integers(0, 256, size=wchunk, dtype=np.uint8)
+
+    srv = socket.create_server(("127.0.0.1", 0))
+    port = srv.getsockname()[1]
+    stats = {"writer": {}, "reader": {}}
+    errors = []
+
+    def timing(d):
+        v = [C.c_double() for _ in range(4)]
+        lib.sg_record_timing(*[C.byref(x) for x in v])
+        for k, x in zip(("h2d_ms", "kernel_ms", "d2h_ms", "host_ms"), v):
+            d[k] = d.get(k, 0.0) + x.value
+
+    def writer():
+        try:
+            enc = ChaCha20Poly1305(args.device).new_encryptor(KEY_C2S)
+            sock = socket.create_connection(("127.0.0.1", port))
+            sock.setsockopt(socket.SOL_SOCKET, socket.SO_SNDBUF, 8 << 20)
+            wire = (C.c_uint8 * lib.sg_wire_bound(wchunk))()
+            src = pattern.ctypes.data_as(C.c_void_p)
+            wl = C.c_size_t(0)
+            seq, sent, t_sock = 0, 0, 0.0
+            d = stats["writer"]
+            while sent < total:
+                n = min(wchunk, total - sent)
+                nrec = N.check(lib.sg_write_records(enc._ptr, seq, 23, 3, 3, src, n, wire, len(wire), C.byref(wl)))
+                timing(d)
+                seq += nrec
+                t0 = time.perf_counter()
+                sock.sendall(memoryview(wire)[:wl.value])
+                t_sock += time.perf_counter() - t0
+                sent += n
+            sock.shutdown(socket.SHUT_WR)
+            d["socket_ms"] = t_sock * 1e3
+            d["records"] = seq
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append(("writer", repr(e)))
+
+    def reader():
+        try:
+            dec = ChaCha20Poly1305(args.device).new_decryptor(KEY_C2S)
+            conn, _ = srv.accept()
+            conn.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 8 << 20)
+            cap = 64 << 20
+            buf = bytearray(cap)
+            mv = memoryview(buf)
+            have = 0
+            out = np.empty(cap, dtype=np.uint8)
+            res = N.SgReadResult()
+            seq, got, t_sock, mism, t_verify = 0, 0, 0.0, 0, 0.0
+            d = stats["reader"]
+            eof = False
+            while not eof:
+                t0 = time.perf_counter()
+                k = conn.recv_into(mv[have:], cap - have)
+                t_sock += time.perf_counter() - t0
+                eof = k == 0
+                have += k
+                if not eof and have < (8 << 20):
+                    continue  # batch up: one device round trip per few MiB
+                if have == 0:
+                    break
+                src = (C.c_uint8 * have).from_buffer(buf)
+                N.check(lib.sg_read_records(dec._ptr, seq, src, have, out.ctypes.data_as(C.c_void_p), cap,
+                                            None, None, 1 << 20, C.byref(res)))
+                del src
+                timing(d)
+                if res.error != N.SG_OK:
+                    raise RuntimeError(f"record error {res.error} after {seq + res.records} records")
+                # verify: the stream is the pattern repeated every wchunk bytes
+                t1 = time.perf_counter()
+                m, a = int(res.out_len), 0
+                while a < m:
+                    off = (got + a) % wchunk
+                    ln = min(m - a, wchunk - off)
+                    if not np.array_equal(out[a:a + ln], pattern[off:off + ln]):
+                        mism += int(np.count_nonzero(out[a:a + ln] != pattern[off:off + ln]))
+                    a += ln
+                got += m
+                t_verify += time.perf_counter() - t1
+                seq += res.records
+                c = int(res.consumed)
+                buf[:have - c] = buf[c:have]
+                have -= c
+            if have:
+                raise RuntimeError(f"{have} trailing bytes")
+            d.update(socket_ms=t_sock * 1e3, verify_ms=t_verify * 1e3, records=seq, bytes=got, mismatched_bytes=mism)
+        except Exception as e:  # pragma: no cover
+            errors.append(("reader", repr(e)))
+
+    t0 = time.perf_counter()
+    tw, tr = threading.Thread(target=writer), threading.Thread(target=reader)
+    tr.start()
+    tw.start()
+    tw.join()
+    tr.join()
+    wall = time.perf_counter() - t0
+    ok = not errors and stats["reader"].get("bytes") == total and stats["reader"].get("mismatched_bytes") == 0
+    print(json.dumps({
+        "config": f"C4: {total} B application stream, TlsWriter/TlsReader batched GPU record layer over "
+                  "loopback TCP, fixed keys (handshake bypassed)",
+        "gib_per_s": round(total / wall / 2**30, 3), "wall_s": round(wall, 3), "correct": ok,
+        "writer": {k: round(v, 1) if isinstance(v, float) else v for k, v in stats["writer"].items()},
+        "reader": {k: round(v, 1) if isinstance(v, float) else v for k, v in stats["reader"].items()},
+        "errors": errors,
+    }))
+    sys.exit(0 if ok else 1)
+
+
+if __name__ == "__main__":
+    main()
