@@ -48,14 +48,16 @@ def hipcc() -> str:
     return str(cand) if cand.exists() else "hipcc"
 
 
-def build_library(force: bool = False) -> Path:
-    """Compile the gfx950 HIP library (seconds)."""
-    if force or _stale(LIB, HIP_DEPS):
-        tmp = LIB.with_suffix(".so.tmp")
+def build_library(force: bool = False, out: Path | None = None, defines=()) -> Path:
+    """Compile the gfx950 HIP library (seconds).  ``out``/``defines`` build an
+    experiment variant (e.g. ``-DSG_SALU_PRE=0``) next to the product library."""
+    target = Path(out) if out else LIB
+    if force or defines or _stale(target, HIP_DEPS):
+        tmp = target.with_suffix(".so.tmp")
         _run([hipcc(), "--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17",
-              "-Wall", "-Wno-unused-result", "-o", str(tmp), *map(str, HIP_SOURCES)])
-        os.replace(tmp, LIB)
-    return LIB
+              "-Wall", "-Wno-unused-result", *defines, "-o", str(tmp), *map(str, HIP_SOURCES)])
+        os.replace(tmp, target)
+    return target
 
 
 def build_oracle(force: bool = False) -> Path:
@@ -68,9 +70,29 @@ def build_oracle(force: bool = False) -> Path:
     return ORACLE_LIB
 
 
+CPP_TEST_SRC = ROOT / "tests" / "cpp" / "test_host.cpp"
+CPP_TEST_BIN = ROOT / "tests" / "cpp" / "test_host"
+CPP_TEST_DEPS = [CPP_TEST_SRC, ROOT / "include" / "suruga" / "cipher.hpp", ROOT / "include" / "suruga" / "tls.hpp",
+                 ROOT / "include" / "suruga_gpu.h", ORACLE_DIR / "suruga_oracle.h"]
+
+
+def build_cpp_tests(force: bool = False) -> Path:
+    """The C++ host-mirror test program (include/suruga/*.hpp), linked against
+    both in-tree libraries."""
+    lib, orc = build_library(), build_oracle()
+    if force or _stale(CPP_TEST_BIN, CPP_TEST_DEPS + [lib, orc]):
+        tmp = CPP_TEST_BIN.with_suffix(".tmp")
+        _run(["g++", "-std=c++17", "-O1", "-Wall", "-Wextra", "-o", str(tmp), str(CPP_TEST_SRC),
+              f"-L{lib.parent}", f"-L{orc.parent}", "-lsuruga_gpu", "-loracle",
+              "-Wl,-rpath,$ORIGIN/../../suruga_amd:$ORIGIN/../../oracle"])
+        os.replace(tmp, CPP_TEST_BIN)
+    return CPP_TEST_BIN
+
+
 def build_all(force: bool = False) -> None:
     build_library(force)
     build_oracle(force)
+    build_cpp_tests(force)
 
 
 if __name__ == "__main__":

@@ -6,6 +6,7 @@ loaded this module raises -- there is no CPU fallback.
 from __future__ import annotations
 
 import ctypes as C
+import os
 import threading
 from pathlib import Path
 
@@ -145,7 +146,9 @@ def load(path: Path | None = None) -> C.CDLL:
     global _lib
     with _lock:
         if _lib is None:
-            p = Path(path) if path else LIB
+            # SURUGA_GPU_LIB: load another build of the same library (A/B kernel
+            # experiments, tools/ab_bench.sh); still the HIP library, never a fallback
+            p = Path(path or os.environ.get("SURUGA_GPU_LIB") or LIB)
             if not p.exists():
                 raise ImportError(
                     f"{p} is missing: build it with `python -m suruga_amd._build` "

@@ -30,6 +30,10 @@
 
 #include <stdint.h>
 
+#ifndef SG_SALU_PRE
+#define SG_SALU_PRE 1  // hoist the counter-free part of ChaCha round 1 to the SALU
+#endif
+
 namespace sg {
 namespace {
 
@@ -66,6 +70,62 @@ __device__ __forceinline__ void chacha_block(uint32_t ks[16], const uint32_t k[8
     uint32_t x12 = ctr, x13 = 0u, x14 = n14, x15 = n15;
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
+        SG_QR(x0, x4, x8, x12) SG_QR(x1, x5, x9, x13) SG_QR(x2, x6, x10, x14) SG_QR(x3, x7, x11, x15)
+        SG_QR(x0, x5, x10, x15) SG_QR(x1, x6, x11, x12) SG_QR(x2, x7, x8, x13) SG_QR(x3, x4, x9, x14)
+    }
+    ks[0] = x0 + 0x61707865u; ks[1] = x1 + 0x3320646eu; ks[2] = x2 + 0x79622d32u; ks[3] = x3 + 0x6b206574u;
+    ks[4] = x4 + k[0]; ks[5] = x5 + k[1]; ks[6] = x6 + k[2]; ks[7] = x7 + k[3];
+    ks[8] = x8 + k[4]; ks[9] = x9 + k[5]; ks[10] = x10 + k[6]; ks[11] = x11 + k[7];
+    ks[12] = x12 + ctr; ks[13] = x13; ks[14] = x14 + n14; ks[15] = x15 + n15;
+}
+
+// ---- uniform-record variant: the counter-free part of round 1 on the SALU ----
+// Within one record only state word 12 (the block counter) differs between
+// blocks.  The column quarter-rounds on words (1,5,9,13), (2,6,10,14),
+// (3,7,11,15) and the first add of (0,4,8,12) are therefore the same for
+// every block; when the record is wave-uniform (key and nonce in SGPRs) they
+// are computed once on the scalar unit, which otherwise idles, instead of
+// costing ~37 VALU per block.  The SALU has no rotate: the opaque asm keeps the
+// shift-or from being matched to v_alignbit.
+__device__ __forceinline__ uint32_t srotl32(uint32_t x, int n) {
+    uint32_t hi = x << n, lo = x >> (32 - n);
+    asm volatile("" : "+s"(hi));
+    return hi | lo;
+}
+#define SG_QR_S(a, b, c, d)                  \
+    a += b; d ^= a; d = srotl32(d, 16);      \
+    c += d; b ^= c; b = srotl32(b, 12);      \
+    a += b; d ^= a; d = srotl32(d, 8);       \
+    c += d; b ^= c; b = srotl32(b, 7);
+
+struct ChaChaPre {
+    uint32_t x[16];  // state after the counter-free part of round 1 (x12 unused)
+};
+
+// k, n14, n15 must be wave-uniform.
+__device__ __forceinline__ ChaChaPre chacha_pre(const uint32_t k[8], uint32_t n14, uint32_t n15) {
+    uint32_t x1 = 0x3320646eu, x2 = 0x79622d32u, x3 = 0x6b206574u;
+    uint32_t x5 = k[1], x6 = k[2], x7 = k[3], x9 = k[5], x10 = k[6], x11 = k[7];
+    uint32_t x13 = 0u, x14 = n14, x15 = n15;
+    SG_QR_S(x1, x5, x9, x13) SG_QR_S(x2, x6, x10, x14) SG_QR_S(x3, x7, x11, x15)
+    return ChaChaPre{{0x61707865u + k[0], x1, x2, x3, k[0], x5, x6, x7, k[4], x9, x10, x11, 0u, x13, x14, x15}};
+}
+
+// Same result as chacha_block(ks, k, ctr, n14, n15), starting from chacha_pre.
+__device__ __forceinline__ void chacha_block_pre(uint32_t ks[16], const ChaChaPre& P, const uint32_t k[8],
+                                                 uint32_t ctr, uint32_t n14, uint32_t n15) {
+    uint32_t x0 = P.x[0], x1 = P.x[1], x2 = P.x[2], x3 = P.x[3];
+    uint32_t x4 = P.x[4], x5 = P.x[5], x6 = P.x[6], x7 = P.x[7];
+    uint32_t x8 = P.x[8], x9 = P.x[9], x10 = P.x[10], x11 = P.x[11];
+    uint32_t x12 = ctr, x13 = P.x[13], x14 = P.x[14], x15 = P.x[15];
+    // rest of round 1, column (0,4,8,12): its first add is in x0 already
+    x12 ^= x0; x12 = rotl32(x12, 16);
+    x8 += x12; x4 ^= x8; x4 = rotl32(x4, 12);
+    x0 += x4; x12 ^= x0; x12 = rotl32(x12, 8);
+    x8 += x12; x4 ^= x8; x4 = rotl32(x4, 7);
+    SG_QR(x0, x5, x10, x15) SG_QR(x1, x6, x11, x12) SG_QR(x2, x7, x8, x13) SG_QR(x3, x4, x9, x14)
+#pragma unroll
+    for (int r = 1; r < 10; ++r) {
         SG_QR(x0, x4, x8, x12) SG_QR(x1, x5, x9, x13) SG_QR(x2, x6, x10, x14) SG_QR(x3, x7, x11, x15)
         SG_QR(x0, x5, x10, x15) SG_QR(x1, x6, x11, x12) SG_QR(x2, x7, x8, x13) SG_QR(x3, x4, x9, x14)
     }
@@ -416,13 +476,17 @@ __device__ __forceinline__ void aead_record(const KParams& p, const uint32_t rec
         // ---- phase 1: keystream XOR, 64 bytes per lane-block ----------------
         const bool vec_ok = (((uintptr_t)in | (uintptr_t)out) & 15u) == 0u;
         const uint32_t nblocks = (n + 63u) >> 6;
+        ChaChaPre pre;
+        if constexpr (SG_SALU_PRE && L >= 64u) pre = chacha_pre(rk.k, rk.n14, rk.n15);
         for (uint32_t b = t; b < nblocks; b += L) {
             const uint32_t off = b << 6;
             if (vec_ok && off + 64u <= n) {
                 const u32x4 d0 = ld16(in + off), d1 = ld16(in + off + 16);
                 const u32x4 d2 = ld16(in + off + 32), d3 = ld16(in + off + 48);
                 uint32_t ks[16];
-                chacha_block(ks, rk.k, b + 1u, rk.n14, rk.n15);  // data uses blocks 1.. (chacha20_poly1305.rs:52)
+                // data uses blocks 1.. (chacha20_poly1305.rs:52)
+                if constexpr (SG_SALU_PRE && L >= 64u) chacha_block_pre(ks, pre, rk.k, b + 1u, rk.n14, rk.n15);
+                else chacha_block(ks, rk.k, b + 1u, rk.n14, rk.n15);
                 const u32x4 r0 = d0 ^ u32x4{ks[0], ks[1], ks[2], ks[3]};
                 const u32x4 r1 = d1 ^ u32x4{ks[4], ks[5], ks[6], ks[7]};
                 const u32x4 r2 = d2 ^ u32x4{ks[8], ks[9], ks[10], ks[11]};
@@ -445,7 +509,8 @@ __device__ __forceinline__ void aead_record(const KParams& p, const uint32_t rec
             } else {
                 // partial last block or misaligned record: byte granular
                 uint32_t ks[16];
-                chacha_block(ks, rk.k, b + 1u, rk.n14, rk.n15);
+                if constexpr (SG_SALU_PRE && L >= 64u) chacha_block_pre(ks, pre, rk.k, b + 1u, rk.n14, rk.n15);
+                else chacha_block(ks, rk.k, b + 1u, rk.n14, rk.n15);
 #pragma unroll
                 for (uint32_t w = 0; w < 16; ++w) {
 #pragma unroll

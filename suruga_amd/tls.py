@@ -33,6 +33,12 @@ RECORD_MAX_LEN = 1 << 14                   # tls.rs:32
 ENC_RECORD_MAX_LEN = (1 << 14) + 2048      # tls.rs:35
 
 
+# alert.rs:5-44: the AlertLevel / AlertDescription values FromPrimitive accepts
+ALERT_LEVELS = frozenset({1, 2})
+ALERT_DESCRIPTIONS = frozenset({0, 10, 20, 21, 22, 30, 40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51, 60, 70, 71,
+                                80, 90, 100, 110})
+
+
 class ContentType(enum.IntEnum):
     """tls.rs:19-29"""
 
@@ -114,6 +120,9 @@ class TlsWriter:
             return
         for off in range(0, len(data), RECORD_MAX_LEN):
             self.write_record(Record(ty, major, minor, bytes(data[off:off + RECORD_MAX_LEN])))
+
+    def write_alert(self, level: int, description: int) -> None:  # tls.rs:154-158
+        self.write_data(ContentType.AlertTy, bytes([level, description]))
 
     def write_change_cipher_spec(self) -> None:  # tls.rs:161-163
         self.write_data(ContentType.ChangeCipherSpecTy, b"\x01")
@@ -200,6 +209,8 @@ class TlsReader:
                     raise TlsError(TlsErrorKind.UnexpectedMessage, "zero-length Alert record arrived")
                 if len(record.fragment) < 2:
                     raise TlsError(TlsErrorKind.UnexpectedMessage, "awkward Alert record arrived")
+                if record.fragment[0] not in ALERT_LEVELS or record.fragment[1] not in ALERT_DESCRIPTIONS:
+                    raise TlsError(TlsErrorKind.UnexpectedMessage, f"unknown alert: {list(record.fragment)}")
                 return ("Alert", (record.fragment[0], record.fragment[1]))
             if ct is ContentType.HandshakeTy:
                 if len(record.fragment) == 0:

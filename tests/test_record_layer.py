@@ -114,6 +114,18 @@ def test_reader_zero_length():
         assert e.value.kind is TlsErrorKind.UnexpectedMessage
 
 
+def test_alert_messages():
+    out = io.BytesIO()
+    w = TlsWriter(out)
+    w.write_alert(2, 20)   # fatal bad_record_mac
+    w.write_alert(2, 99)   # not an AlertDescription (alert.rs:13-44)
+    r = TlsReader(io.BytesIO(out.getvalue()))
+    assert r.read_message() == ("Alert", (2, 20))
+    with pytest.raises(TlsError) as e:
+        r.read_message()
+    assert e.value.kind is TlsErrorKind.UnexpectedMessage
+
+
 def test_writer_too_long():
     class Enc(Encryptor):
         def encrypt(self, nonce, fragment, ad):
