@@ -287,9 +287,10 @@ static int single(sg_ctx* c, bool open, const uint8_t* nonce, size_t nonce_len, 
     if (!c) return fail(SG_E_ARG, "context is NULL%s");
     if (nonce_len != SG_NONCE_LEN || !nonce) return fail(SG_E_ARG, "nonce must be 8 bytes%s");
     if (adlen > SG_MAX_AD_LEN || (adlen && !ad)) return fail(SG_E_ARG, "bad additional data%s");
-    if ((in_len && !in) || !out) return fail(SG_E_ARG, "NULL buffer%s");
+    if (in_len && !in) return fail(SG_E_ARG, "NULL buffer%s");
     if (open && in_len < SG_MAC_LEN) return SG_E_SHORT;  // chacha20_poly1305.rs:68-70
     const size_t n = open ? in_len - SG_MAC_LEN : in_len;
+    if (!out && (open ? n : n + SG_MAC_LEN)) return fail(SG_E_ARG, "NULL buffer%s");  // empty pt: out may be NULL
     if (n > SG_MAX_RECORD_LEN) return fail(SG_E_ARG, "record longer than SG_MAX_RECORD_LEN%s");
 
     std::lock_guard<std::mutex> lk(c->mu);
