@@ -211,6 +211,33 @@ int sg_read_records(sg_ctx* ctx, uint64_t seq0, const uint8_t* wire, size_t wire
  * summed over the pipelined chunks) and in host-side framing memcpy. */
 int sg_record_timing(double* h2d_ms, double* kernel_ms, double* d2h_ms, double* host_ms);
 
+/* ---- TLS 1.2 key schedule on the host (cipher/prf.rs, client.rs:130-225) --
+ * Produces the per-connection key tables the batch calls take.  CPU only
+ * (no device needed); the reference's hmac_sha256 panics for keys longer than
+ * 64 bytes (prf.rs:11-14): SG_E_ARG here. */
+void sg_sha256(const uint8_t* msg, size_t len, uint8_t out[32]);          /* crypto/sha2.rs:18-116 */
+int  sg_hmac_sha256(const uint8_t* key, size_t key_len, const uint8_t* msg, size_t len,
+                    uint8_t out[32]);                                     /* prf.rs:8-29          */
+typedef struct sg_prf sg_prf;                                             /* prf.rs:31-36 Prf     */
+sg_prf* sg_prf_new(const uint8_t* secret, size_t secret_len,
+                   const uint8_t* seed, size_t seed_len);                 /* prf.rs:38-48         */
+int  sg_prf_get_bytes(sg_prf* prf, uint8_t* out, size_t n);               /* prf.rs:60-89         */
+void sg_prf_free(sg_prf* prf);
+/* client.rs:130-163 for `count` connections (threads >= 1):
+ *   master_secret_i = PRF(pre_master_i, "master secret" || client_random_i || server_random_i)[0..48]
+ *   key block = PRF(master_secret_i, "key expansion" || server_random_i || client_random_i)
+ *   client_write_key_i = key block[0..32] (the client's encryptor key, client.rs:152-154)
+ *   server_write_key_i = key block[32..64] (the client's decryptor key, :157)
+ * pre_master_i = pre_master + pm_stride*i (pm_len bytes); randoms are [count][32];
+ * master_secret ([count][48]) may be NULL. */
+int  sg_derive_keys(uint32_t count, const uint8_t* pre_master, size_t pm_len, size_t pm_stride,
+                    const uint8_t* client_random, const uint8_t* server_random, uint8_t* master_secret,
+                    uint8_t* client_write_keys, uint8_t* server_write_keys, int threads);
+/* client.rs:184-192 (server = 0, "client finished") / :213-221 (server = 1,
+ * "server finished"): PRF(master_secret, label || handshake_hash)[0..12]. */
+int  sg_finished_verify_data(const uint8_t master_secret[48], int server,
+                             const uint8_t handshake_hash[32], uint8_t out[12]);
+
 /* ---- synthetic workload helpers (bench / tests) ------------------------ */
 /* Fills records on the device: byte i of record j =
  * byte (i mod 8) of splitmix64(seed ^ ((j0 + j) << 32) ^ (i / 8)).

@@ -23,7 +23,7 @@ LIB = PKG / "libsuruga_gpu.so"
 ORACLE_DIR = ROOT / "oracle"
 ORACLE_LIB = ORACLE_DIR / "liboracle.so"
 
-HIP_SOURCES = [CSRC / "sg_kernels.hip", CSRC / "sg_capi.cpp", CSRC / "sg_record.cpp"]
+HIP_SOURCES = [CSRC / "sg_kernels.hip", CSRC / "sg_capi.cpp", CSRC / "sg_record.cpp", CSRC / "sg_keysched.cpp"]
 HIP_DEPS = HIP_SOURCES + [CSRC / "sg_internal.h", CSRC / "sg_host.h", ROOT / "include" / "suruga_gpu.h"]
 ORACLE_SOURCES = [ORACLE_DIR / "suruga_oracle.c"]
 ORACLE_DEPS = ORACLE_SOURCES + [ORACLE_DIR / "suruga_oracle.h"]
@@ -73,6 +73,7 @@ def build_oracle(force: bool = False) -> Path:
 CPP_TEST_SRC = ROOT / "tests" / "cpp" / "test_host.cpp"
 CPP_TEST_BIN = ROOT / "tests" / "cpp" / "test_host"
 CPP_TEST_DEPS = [CPP_TEST_SRC, ROOT / "include" / "suruga" / "cipher.hpp", ROOT / "include" / "suruga" / "tls.hpp",
+                 ROOT / "include" / "suruga" / "prf.hpp",
                  ROOT / "include" / "suruga_gpu.h", ORACLE_DIR / "suruga_oracle.h"]
 
 

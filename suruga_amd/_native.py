@@ -34,6 +34,8 @@ EXPORTS = [
     "sg_fill_records", "sg_compare_records",
     "sg_last_error", "sg_build_info", "sg_set_timing", "sg_timing_read",
     "sg_wire_bound", "sg_write_records", "sg_read_records", "sg_record_timing",
+    "sg_sha256", "sg_hmac_sha256", "sg_prf_new", "sg_prf_get_bytes", "sg_prf_free",
+    "sg_derive_keys", "sg_finished_verify_data",
 ]
 
 
@@ -139,6 +141,21 @@ def _declare(lib: C.CDLL) -> None:
                                     C.c_void_p, C.c_void_p, C.c_size_t, C.POINTER(SgReadResult)]
     lib.sg_record_timing.restype = C.c_int
     lib.sg_record_timing.argtypes = [d, d, d, d]
+    vp = C.c_void_p
+    lib.sg_sha256.restype = None
+    lib.sg_sha256.argtypes = [vp, C.c_size_t, vp]
+    lib.sg_hmac_sha256.restype = C.c_int
+    lib.sg_hmac_sha256.argtypes = [vp, C.c_size_t, vp, C.c_size_t, vp]
+    lib.sg_prf_new.restype = vp
+    lib.sg_prf_new.argtypes = [vp, C.c_size_t, vp, C.c_size_t]
+    lib.sg_prf_get_bytes.restype = C.c_int
+    lib.sg_prf_get_bytes.argtypes = [vp, vp, C.c_size_t]
+    lib.sg_prf_free.restype = None
+    lib.sg_prf_free.argtypes = [vp]
+    lib.sg_derive_keys.restype = C.c_int
+    lib.sg_derive_keys.argtypes = [C.c_uint32, vp, C.c_size_t, C.c_size_t, vp, vp, vp, vp, vp, C.c_int]
+    lib.sg_finished_verify_data.restype = C.c_int
+    lib.sg_finished_verify_data.argtypes = [vp, C.c_int, vp, vp]
 
 
 def load(path: Path | None = None) -> C.CDLL:

@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "../../include/suruga/cipher.hpp"
+#include "../../include/suruga/prf.hpp"
 #include "../../include/suruga/tls.hpp"
 #include "../../oracle/suruga_oracle.h"
 
@@ -181,6 +182,42 @@ static void cpu_tests() {
         TlsReader r(in);
         r.set_decryptor(std::make_unique<OracleDecryptor>(key_seq(0)));
         CHECK(r.read_application_data() == Bytes(16, 'A'));
+    }
+    {  // prf.rs:137-166 test_get_bytes and prf.rs:98-132 (RFC 4231 case 2)
+        Prf p1{Slice(), Slice()};
+        Bytes r1;
+        for (int i = 0; i < 100; ++i) {
+            Bytes b = p1.get_bytes(1);
+            r1.insert(r1.end(), b.begin(), b.end());
+        }
+        Prf p3{Slice(), Slice()};
+        Bytes r3 = p3.get_bytes(33);
+        Bytes b2 = p3.get_bytes(33);
+        Bytes b3 = p3.get_bytes(34);
+        r3.insert(r3.end(), b2.begin(), b2.end());
+        r3.insert(r3.end(), b3.begin(), b3.end());
+        Prf p2{Slice(), Slice()};
+        CHECK(r1 == p2.get_bytes(100) && r1 == r3);
+        const std::string jefe = "Jefe", msg = "what do ya want for nothing?";
+        auto h = hmac_sha256(Slice(reinterpret_cast<const uint8_t*>(jefe.data()), jefe.size()),
+                             Slice(reinterpret_cast<const uint8_t*>(msg.data()), msg.size()));
+        CHECK(hex(h.data(), 32) == "5bdcc146bf60754e6a042426089575c75a003f089d2739839dec58b964ec3843");
+        auto e = sha256(Slice());
+        CHECK(hex(e.data(), 32) == "e3b0c44298fc1c149afbf4c8996fb92427ae41e4649b934ca495991b7852b855");
+        uint8_t cr[32], sr[32];
+        for (int i = 0; i < 32; ++i) cr[i] = (uint8_t)i, sr[i] = (uint8_t)(100 + i);
+        Bytes pm(32, 7);
+        ConnectionKeys k = derive_keys(pm, cr, sr);
+        Bytes seed(13 + 64);
+        std::memcpy(seed.data(), "master secret", 13);
+        std::memcpy(seed.data() + 13, cr, 32);
+        std::memcpy(seed.data() + 45, sr, 32);
+        CHECK(k.master_secret == Prf(pm, seed).get_bytes(48));
+        std::memcpy(seed.data(), "key expansion", 13);
+        std::memcpy(seed.data() + 13, sr, 32);
+        std::memcpy(seed.data() + 45, cr, 32);
+        Prf kb(k.master_secret, seed);
+        CHECK(k.client_write_key == kb.get_bytes(32) && k.server_write_key == kb.get_bytes(32));
     }
     {  // cipher suite registration (mod.rs:108-114) and Aead constants (chacha20_poly1305.rs:102-119)
         auto aead = new_aead(TLS_ECDHE_RSA_WITH_CHACHA20_POLY1305_SHA256);

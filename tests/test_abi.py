@@ -18,7 +18,7 @@ HEADER = ROOT / "include" / "suruga_gpu.h"
 def declared_symbols():
     text = HEADER.read_text()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return sorted(set(re.findall(r"\b(sg_[a-z_]+)\s*\(", text)))
+    return sorted(set(re.findall(r"\b(sg_[a-z0-9_]+)\s*\(", text)))
 
 
 @pytest.fixture(scope="module")
