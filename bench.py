@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=4096, help="records in the CPU-baseline sample")
     ap.add_argument("--cpu-seconds", type=float, default=2.0, help="min wall time of the CPU baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--strong", action="store_true",
+                    help="strong scaling: --records in total, split across ranks (default: weak, per rank)")
     ap.add_argument("--traffic", default=str(ROOT / "profiles" / "traffic_r01.json"),
                     help="PMC-derived HBM traffic summary (tools/pmc_traffic.py)")
     return ap.parse_args()
@@ -88,6 +90,16 @@ def cpu_baseline(args, n):
     }
 
 
+def sum_over_ranks(dist, value, device=None):
+    if dist is None:
+        return value
+    import torch
+
+    t = torch.tensor([float(value)], dtype=torch.float64, device=device)
+    dist.all_reduce(t)
+    return float(t.item())
+
+
 def main():
     args = parse()
     import torch
@@ -96,20 +108,31 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # one process per GPU; the process group only carries the timing protocol
+    # (barriers + MAX of the elapsed time): RCCL ("nccl") by default, gloo for
+    # rehearsing several ranks on one card (SG_DIST_BACKEND=gloo)
+    backend = os.environ.get("SG_DIST_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    local_dev = local % ndev if ndev else local
+    torch.cuda.set_device(local_dev)
+    dev = torch.device("cuda", local_dev)
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+        dist.init_process_group(backend, device_id=dev if backend == "nccl" else None)
 
     from suruga_amd import _build
     from suruga_amd import batch as B
+    from suruga_amd import shard
 
     if not _build.LIB.exists():
         _build.build_library()
-    n, count = args.record_bytes, args.records
-    seq0 = rank * count
+    n = args.record_bytes
+    if args.strong:  # total work fixed: rank r owns a contiguous slice of --records
+        lo, hi = shard.record_range(args.records, rank, world)
+        count, seq0 = hi - lo, lo
+    else:            # weak scaling (the metric's mode): --records per rank, seq r*records + i
+        count, seq0 = args.records, rank * args.records
     stream = torch.cuda.current_stream(dev)
     ws = torch.empty(B.workspace_size(count), dtype=torch.uint8, device=dev)
     status = torch.empty(count, dtype=torch.uint8, device=dev)
@@ -165,21 +188,8 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = shard.timed(dist, step, args.steps, sync=torch.cuda.synchronize,
+                          device=dev if backend == "nccl" else None)
 
     # correctness of the last step (outside the timed region)
     mism = torch.zeros(1, dtype=torch.int64, device=dev)
@@ -194,7 +204,10 @@ def main():
     tm = B.timing_read()
     B.set_timing(False)
 
-    payload = payload_per_step * args.steps * world  # seal + open plaintext bytes, all ranks
+    # seal + open plaintext bytes of all ranks (weak: every rank the same count)
+    total_payload_per_step = payload_per_step * world if not args.strong else int(
+        sum_over_ranks(dist, payload_per_step, dev if backend == "nccl" else None))
+    payload = total_payload_per_step * args.steps
     value = payload / elapsed / 2**30
     ms_per_step = elapsed / args.steps * 1e3
 
@@ -221,7 +234,7 @@ def main():
         line = {
             "metric": METRIC, "value": round(value, 3), "unit": "GiB/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+            "higher_is_better": True, "scaling": "strong" if args.strong else "weak", "vs_baseline": None, "dtype": "u32",
             "data": "synthetic (splitmix64 records generated on device)",
             "config": dict(cfg, parallelism=f"record-shard x{world}", kernels=lib.sg_build_info().decode()),
             "roofline": {"bound": "hbm", "kernel": f"sg_aead_kernel<{'OPEN' if dom == 'open' else 'SEAL'}>",
@@ -230,7 +243,7 @@ def main():
                          "alg_bytes_per_launch": alg_bytes, "avg_launch_ms": round(dom_ms, 4)},
             "kernel_ms": {"seal": round(tm["seal_ms"], 4), "open": round(tm["open_ms"], 4),
                           "keying": round(tm["keying_ms"], 4)},
-            "records_per_s": round(count * world * args.steps / elapsed, 1),
+            "records_per_s": round((args.records if args.strong else count * world) * args.steps / elapsed, 1),
             "correct": roundtrip_ok,
             "cpu_baseline": cpu,
         }

@@ -1,0 +1,62 @@
+"""bench.py's output contract and its multi-rank path.  CPU: argument parsing
+only.  GPU: a small N=1 run and an N=2 run launched the way the driver launches
+it (torch.distributed.run, 127.0.0.1), both ranks on the one card of the test
+box with the gloo process group (RCCL needs one device per rank)."""
+from __future__ import annotations
+
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+        "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"}
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _last_json(out: str):
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out
+    return json.loads(lines[0])
+
+
+def test_bench_help():
+    p = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--help"], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0 and "--gpus" in p.stdout and "--strong" in p.stdout
+
+
+@pytest.mark.gpu
+def test_bench_single_gpu_small(gpu):
+    p = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--records", "4096", "--steps", "2", "--warmup", "1",
+                        "--no-cpu-baseline"], capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    j = _last_json(p.stdout)
+    assert KEYS <= set(j) and j["n_gpus"] == 1 and j["correct"] and j["value"] > 0
+    assert set(j["roofline"]) >= {"bound", "achieved", "peak", "unit", "frac", "traffic"}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("strong", [False, True])
+def test_bench_two_ranks_one_card(gpu, strong):
+    env = dict(os.environ, SG_DIST_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), str(ROOT / "bench.py"), "--gpus", "2",
+           "--records", "4096", "--steps", "2", "--warmup", "1", "--no-cpu-baseline"] + (["--strong"] if strong else [])
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    j = _last_json(p.stdout)
+    assert j["n_gpus"] == 2 and j["correct"] and j["scaling"] == ("strong" if strong else "weak")
+    if strong:
+        assert j["records_per_s"] * j["ms_per_step"] / 1e3 == pytest.approx(4096, rel=1e-3)
+    else:
+        assert j["records_per_s"] * j["ms_per_step"] / 1e3 == pytest.approx(8192, rel=1e-3)
