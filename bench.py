@@ -26,6 +26,9 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak, /opt/skills/guides/MI355X_MICROARCH.md
+# VALU issue peak: 1024 SIMDs x one wave64 instruction per 2 cycles x 2.4 GHz (same guide);
+# streams mixing ALU kinds issue at ~4 cycles on gfx950 (tools/valu_probe*.hip)
+VALU_PEAK_GIPS = 1024 * 0.5 * 2.4
 SEED = 0x53555255
 KEY = bytes(range(32))
 METRIC = "GiB/s device-resident ChaCha20-Poly1305 over 16 KiB TLS records, 1/2/4/8 GPUs"
@@ -45,7 +48,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--strong", action="store_true",
                     help="strong scaling: --records in total, split across ranks (default: weak, per rank)")
-    ap.add_argument("--traffic", default=str(ROOT / "profiles" / "traffic_r01.json"),
+    ap.add_argument("--traffic", default=None,
                     help="PMC-derived HBM traffic summary (tools/pmc_traffic.py)")
     return ap.parse_args()
 
@@ -217,13 +220,25 @@ def main():
     alg_bytes = alg[dom]
     dom_ms = tm[f"{dom}_ms"]
     achieved = alg_bytes / (dom_ms * 1e-3) / 1e9
-    traffic = None
-    tp = Path(args.traffic)
+    traffic, valu = None, None
+    tp = Path(args.traffic or ROOT / "profiles" / ("traffic_r01.json" if args.workload == "c1" else
+                                                   "traffic_r01_c2.json"))
     if tp.exists():
         try:
             tj = json.loads(tp.read_text())
-            if tj.get("records") == count and tj.get("record_bytes") == cfg["record_bytes"]:
+            if tj.get("records") == count and tj.get("record_bytes") == cfg["record_bytes"] and \
+                    tj.get("kernels", lib.sg_build_info().decode()) == lib.sg_build_info().decode():
                 traffic = tj.get(f"{dom}_bytes_per_launch")
+                vpr = tj.get(f"{dom}_valu_per_record")
+                if vpr:
+                    # VALU issue account of the same kernel: PMC SQ_INSTS_VALU per record (a
+                    # property of the code, from the profile) / this run's launch time
+                    ips = vpr * count / (dom_ms * 1e-3)
+                    valu = {"bound": "valu", "instr_per_record": round(vpr, 1),
+                            "achieved": round(ips / 1e9, 1), "unit": "G wave-instr/s",
+                            "peak": VALU_PEAK_GIPS, "frac": round(ips / 1e9 / VALU_PEAK_GIPS, 4),
+                            "peak_mixed_stream": VALU_PEAK_GIPS / 2,
+                            "frac_mixed_stream": round(ips / 1e9 / (VALU_PEAK_GIPS / 2), 4)}
         except (ValueError, OSError):
             traffic = None
 
@@ -241,6 +256,7 @@ def main():
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "alg_bytes_per_launch": alg_bytes, "avg_launch_ms": round(dom_ms, 4)},
+            "valu_roofline": valu,
             "kernel_ms": {"seal": round(tm["seal_ms"], 4), "open": round(tm["open_ms"], 4),
                           "keying": round(tm["keying_ms"], 4)},
             "records_per_s": round((args.records if args.strong else count * world) * args.steps / elapsed, 1),

@@ -228,8 +228,8 @@ int sg_abi_version(void) { return SG_ABI_VERSION; }
 const char* sg_last_error(void) { return g_err.c_str(); }
 const char* sg_build_info(void) { return sg::kernel_config(); }
 size_t sg_workspace_size(uint32_t count) {
-    // keying records, one list per size class, four list counters
-    return (size_t)count * (sg::kKeyRecWords + sg::kNumClasses) * 4u + 16u;
+    // keying records, one list per size class, one list counter per class
+    return (size_t)count * (sg::kKeyRecWords + sg::kNumClasses) * 4u + sg::kNumClasses * 4u;
 }
 
 sg_ctx* sg_ctx_new(const uint8_t key[32], int device) {

@@ -47,28 +47,32 @@ struct KParams {
     uint32_t pad;
 };
 
-// Size classes of the AEAD kernel: lanes per record L = 16 (n <= 1 KiB),
-// 64 (n <= 4 KiB), 128 (n <= 8 KiB) or 256; MAC lanes PL = min(L, 64).
-// Records of mixed sizes are bucketed on the device (sg_classify_kernel).
-constexpr uint32_t kNumClasses = 4;
-constexpr uint32_t kClass0Max = 1024;
-constexpr uint32_t kClass1Max = 4096;
-constexpr uint32_t kClass2Max = 8192;
+// Size classes of the AEAD kernel: class c (0..7) holds records of
+// n <= 128 << c bytes (class 7: the rest, up to SG_MAX_RECORD_LEN) and gives
+// each record L = 2 << c lanes, one 64-byte ChaCha20 block per lane for
+// c < 7; the MAC runs on PL = min(L, 64) lanes.  A 256-thread workgroup serves
+// 256 / L records.  Mixed sizes are bucketed on the device (sg_classify_kernel).
+constexpr uint32_t kNumClasses = 8;
 constexpr uint32_t kListGridPerCU = 8;   // workgroups per CU for list-driven launches
 
 __host__ __device__ inline uint32_t size_class(uint32_t n) {
-    return n <= kClass0Max ? 0u : (n <= kClass1Max ? 1u : (n <= kClass2Max ? 2u : 3u));
+    if (n <= 128u) return 0u;
+    const uint32_t c = 32u - (uint32_t)__builtin_clz((n - 1u) >> 7);
+    return c < 7u ? c : 7u;
 }
+__host__ __device__ constexpr uint32_t class_lanes(uint32_t c) { return 2u << c; }
+__host__ __device__ constexpr uint32_t class_mac_lanes(uint32_t c) { return class_lanes(c) < 64u ? class_lanes(c) : 64u; }
+__host__ __device__ constexpr uint32_t class_max(uint32_t c) { return c < 7u ? 128u << c : 0xffffffffu; }
 // LDS bytes of one record slot: zero region (16 bytes x max virtual blocks
 // 2*PL) | ad || le64 (16-rounded) | ct (64-rounded) | le64(n) + zeros + funnel slack
 __host__ __device__ inline uint32_t lds_rec_bytes(uint32_t cls, uint32_t adlen, uint32_t max_n) {
-    const uint32_t PL = cls == 0 ? 16u : 64u;
+    const uint32_t PL = class_mac_lanes(cls);
     return 32u * PL + ((adlen + 8u + 15u) & ~15u) + ((max_n + 63u) & ~63u) + 64u;
 }
 
 hipError_t launch_keying(const KParams& p, bool open, hipStream_t s);
 // Seal/open launch.  uniform: every record is in size_class(max_n) (direct
-// launch); otherwise classify into lists[kNumClasses][count] / counts[4] and
+// launch); otherwise classify into lists[kNumClasses][count] / counts[kNumClasses] and
 // launch per class.
 hipError_t launch_aead(const KParams& p, bool open, uint32_t max_n, bool uniform, uint32_t* lists,
                        uint32_t* counts, hipStream_t s);

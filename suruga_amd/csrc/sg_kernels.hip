@@ -324,7 +324,7 @@ __device__ __forceinline__ MacGeom mac_geom(uint32_t adlen, uint32_t n, uint32_t
 
 // MAC lanes per record, a function of the payload length only so that the
 // keying kernel and every AEAD size class agree on k (see size_class).
-__device__ __forceinline__ uint32_t mac_lanes(uint32_t n) { return n <= kClass0Max ? 16u : 64u; }
+__device__ __forceinline__ uint32_t mac_lanes(uint32_t n) { return class_mac_lanes(size_class(n)); }
 
 // Per-record parameters shared by the keying and AEAD kernels.
 struct RecKey {
@@ -532,7 +532,7 @@ __device__ __forceinline__ void aead_record(const KParams& p, const uint32_t rec
             const u32x4 zero = {0u, 0u, 0u, 0u};
             st16(lds + 16u * t, zero);  // [0, Z): virtual blocks read zeros
             st16(lds + 16u * (t + PL), zero);
-            if (Z + t < S) lds[Z + t] = 0;
+            for (uint32_t i = Z + t; i < S; i += PL) lds[i] = 0;  // gap before the stream start
             for (uint32_t i = t; i < adlen + 8u; i += PL) {
                 uint8_t v;
                 if (i < adlen)
@@ -700,7 +700,7 @@ __global__ __launch_bounds__(1024) void sg_classify_kernel(const KParams p, uint
     const uint32_t lane = __lane_id(), wave = threadIdx.x >> 6;
     const uint32_t rec0 = blockIdx.x * (kClassifyThreads * kClassifyPerThread);
     uint32_t cls[kClassifyPerThread];
-    uint32_t mine[kNumClasses] = {0u, 0u, 0u, 0u};  // this wave's records per class
+    uint32_t mine[kNumClasses] = {};  // this wave's records per class
 #pragma unroll
     for (uint32_t i = 0; i < kClassifyPerThread; ++i) {
         const uint32_t rec = rec0 + i * kClassifyThreads + threadIdx.x;
@@ -826,39 +826,42 @@ hipError_t launch_list(const KParams& p, const uint32_t* list, const uint32_t* c
 }
 
 template <bool OPEN>
+hipError_t launch_class(uint32_t c, const KParams& q, const uint32_t* list, const uint32_t* cnt, hipStream_t s) {
+#define SG_CLASS_CASE(C)                                                                  \
+    case C:                                                                               \
+        return list ? launch_list<OPEN, class_lanes(C)>(q, list, cnt, s)                  \
+                    : launch_direct<OPEN, class_lanes(C)>(q, s);
+    switch (c) {
+        SG_CLASS_CASE(0) SG_CLASS_CASE(1) SG_CLASS_CASE(2) SG_CLASS_CASE(3)
+        SG_CLASS_CASE(4) SG_CLASS_CASE(5) SG_CLASS_CASE(6)
+        default: return list ? launch_list<OPEN, class_lanes(7)>(q, list, cnt, s)
+                             : launch_direct<OPEN, class_lanes(7)>(q, s);
+    }
+#undef SG_CLASS_CASE
+}
+
+template <bool OPEN>
 hipError_t launch_aead_t(const KParams& p, uint32_t max_n, bool uniform, uint32_t* lists, uint32_t* counts,
                          hipStream_t s) {
     if (uniform) {  // every record in one class: direct launch
         KParams q = p;
         const uint32_t c = size_class(max_n);
         q.lds_rec_bytes = lds_rec_bytes(c, q.ad_len, max_n);
-        switch (c) {
-            case 0: return launch_direct<OPEN, 16>(q, s);
-            case 1: return launch_direct<OPEN, 64>(q, s);
-            case 2: return launch_direct<OPEN, 128>(q, s);
-            default: return launch_direct<OPEN, 256>(q, s);
-        }
+        return launch_class<OPEN>(c, q, nullptr, nullptr, s);
     }
-    hipError_t e = hipMemsetAsync(counts, 0, 16, s);
+    hipError_t e = hipMemsetAsync(counts, 0, kNumClasses * sizeof(uint32_t), s);
     if (e != hipSuccess) return e;
     const uint32_t per_wg = kClassifyThreads * kClassifyPerThread;
     hipLaunchKernelGGL(sg_classify_kernel<OPEN>, dim3((p.count + per_wg - 1u) / per_wg), dim3(kClassifyThreads), 0, s,
                        p, lists, counts);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    // one launch per populated class, largest records first
-    static const uint32_t class_max[kNumClasses] = {kClass0Max, kClass1Max, kClass2Max, 0xffffffffu};
+    // one launch per possibly populated class, largest records first
     KParams q = p;
     for (int c = (int)size_class(max_n); c >= 0; --c) {
-        const uint32_t cap = max_n < class_max[c] ? max_n : class_max[c];
+        const uint32_t cap = max_n < class_max((uint32_t)c) ? max_n : class_max((uint32_t)c);
         q.lds_rec_bytes = lds_rec_bytes((uint32_t)c, q.ad_len, cap);
-        const uint32_t* list = lists + (uint64_t)c * p.count;
-        switch (c) {
-            case 0: e = launch_list<OPEN, 16>(q, list, counts + 0, s); break;
-            case 1: e = launch_list<OPEN, 64>(q, list, counts + 1, s); break;
-            case 2: e = launch_list<OPEN, 128>(q, list, counts + 2, s); break;
-            default: e = launch_list<OPEN, 256>(q, list, counts + 3, s); break;
-        }
-        if (e != hipSuccess) return e;
+        if ((e = launch_class<OPEN>((uint32_t)c, q, lists + (uint64_t)c * p.count, counts + c, s)) != hipSuccess)
+            return e;
     }
     return hipSuccess;
 }
@@ -888,8 +891,11 @@ hipError_t launch_compare(const uint8_t* a, uint64_t sa, const uint8_t* b, uint6
 }
 
 const char* kernel_config() {
-    return "gfx950 sg_aead_kernel v4: size classes (16/64/128/256 lanes per record, device bucketing), "
-           "lane=64B ChaCha block, Poly1305 contiguous-chunk Horner radix-2^32 (clamped r) on 16/64 lanes + "
+#define SG_STR2(x) #x
+#define SG_STR(x) SG_STR2(x)
+    return "gfx950 sg_aead_kernel v6" "/salu_pre=" SG_STR(SG_SALU_PRE)
+           ": 8 size classes (2..256 lanes per record, one 64-B block per lane, device bucketing), "
+           "lane=64B ChaCha block (counter-free round-1 QRs on SALU for wave-uniform records), Poly1305 contiguous-chunk Horner radix-2^32 (clamped r) on min(L,64) lanes + "
            "per-lane r^(k(PL-1-t)) scale + shuffle sum, keying pre-pass";
 }
 

@@ -145,8 +145,9 @@ def test_c1_subset_4096_x_16kib_bit_exact(gpu, oracle):
     assert host(back) == pt_h and host(st) == bytes(count)
 
 
-@pytest.mark.parametrize("n", [0, 1, 15, 16, 17, 63, 64, 65, 100, 255, 256, 1000, 1024, 1025, 4095, 4096, 4097,
-                               5000, 8192, 8193, 16383, 16384, 18432])
+@pytest.mark.parametrize("n", [0, 1, 15, 16, 17, 63, 64, 65, 100, 127, 128, 129, 255, 256, 257, 511, 512, 513,
+                               1000, 1024, 1025, 2047, 2048, 2049, 4095, 4096, 4097, 5000, 8192, 8193, 16383,
+                               16384, 18432])
 def test_batch_lengths(gpu, oracle, n):
     count = 33
     pt, ct, back, st = tls_batch(count, n, seq0=0xFFFFFFF0)
@@ -230,13 +231,16 @@ def test_batch_ragged_offsets_keys_and_tamper(gpu, oracle):
         assert back_h[in_off[i]:in_off[i] + lens[i]] == pt_h[in_off[i]:in_off[i] + lens[i]], i
 
 
-def test_batch_explicit_mode(gpu, oracle):
+@pytest.mark.parametrize("n", [5, 100, 200, 400, 777, 3000])
+def test_batch_explicit_mode(gpu, oracle, n):
+    """Explicit nonce/AD of every length class; small n puts 2..8 MAC lanes on
+    a record, so the zero gap before the MAC stream spans several lanes' bytes."""
     torch = torch_mod()
     from suruga_amd import batch as B
 
-    rng = np.random.default_rng(3)
-    for adlen in (0, 5, 13, 32, 255):
-        count, n = 40, 777
+    rng = np.random.default_rng(3 + n)
+    for adlen in (0, 1, 5, 13, 17, 32, 255):
+        count = 40
         nonces_h, ads_h, pt_h = rng.bytes(8 * count), rng.bytes(max(adlen, 1) * count), rng.bytes(n * count)
         keys = dev_bytes(KEY).view(1, 32)
         ct = torch.empty(count * (n + 16), dtype=torch.uint8, device="cuda")
@@ -277,15 +281,15 @@ def test_c1_scale_roundtrip_and_tag_fold(gpu, oracle):
 
 def test_c2_zipf_sample_bit_exact(gpu, oracle):
     """C2 shape: Zipf 64 B-16 KiB, 256 connection keys, seq = i / 256; mixed
-    sizes go through device bucketing into all three size classes."""
+    sizes go through device bucketing into all eight size classes."""
     torch = torch_mod()
     from suruga_amd import batch as B
     from suruga_amd import workloads as W
 
     count = 3000
     lay = W.c2_layout(count)
-    classes = {(int(x) > 1024) + (int(x) > 4096) + (int(x) > 8192) for x in lay.lens}
-    assert classes == {0, 1, 2, 3}
+    classes = {0 if int(x) <= 128 else min(7, ((int(x) - 1) >> 7).bit_length()) for x in lay.lens}
+    assert classes == set(range(8))  # include/suruga_gpu.h size classes: n <= 128 << c
     rng = np.random.default_rng(5)
     pt_h = rng.bytes(lay.pt_bytes)
     t64 = lambda a: torch.from_numpy(a.view(np.int64)).to("cuda")

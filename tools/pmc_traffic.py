@@ -17,6 +17,7 @@ from __future__ import annotations
 import collections
 import csv
 import json
+import re
 import shutil
 import sys
 from pathlib import Path
@@ -25,11 +26,13 @@ ROOT = Path(__file__).resolve().parent.parent
 
 
 def kind(name: str):
-    if "aead_kernel<false>" in name or "seal" in name and "sg_" in name:
-        return "seal"
-    if "aead_kernel<true>" in name or "open" in name and "sg_" in name:
-        return "open"
-    for k in ("keying", "compare", "fill"):
+    m = re.search(r"aead(?:_list)?_kernel<(false|true)", name)
+    if m:
+        return "seal" if m.group(1) == "false" else "open"
+    m = re.search(r"(keying|classify)_kernel<(false|true)", name)
+    if m:
+        return f"{m.group(1)}_{'seal' if m.group(2) == 'false' else 'open'}"
+    for k in ("compare", "fill"):
         if k in name:
             return k
     return None
@@ -42,15 +45,46 @@ def main(tag: str, records: int = 1 << 20, record_bytes: int = 16384):
     ks = src / "kt" / "run_kernel_stats.csv"
     if ks.exists():
         shutil.copy(ks, dst / f"{tag}_kernel_stats.csv")
-    acc = collections.defaultdict(lambda: collections.defaultdict(list))
+    # Per BATCH (one sg_seal_batch / sg_open_batch call) sums: a mixed-size batch
+    # launches classify + one list kernel per size class; a batch is counted by
+    # its keying dispatch.  For C1 a batch is exactly one aead kernel launch.
+    acc = collections.defaultdict(lambda: collections.defaultdict(float))
+    nbatch = collections.defaultdict(lambda: collections.defaultdict(int))
     for f in sorted(src.glob("pmc_*/run_counter_collection.csv")):
+        seen = set()
         for r in csv.DictReader(open(f)):
             k = kind(r["Kernel_Name"])
             if not k:
                 continue
-            acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
-            acc[k]["dispatch_ns"].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
-    summ = {k: {c: sum(v) / len(v) for c, v in d.items()} for k, d in acc.items()}
+            acc[k][r["Counter_Name"]] += float(r["Counter_Value"])
+            nbatch[k][r["Counter_Name"]] += 0
+            key = (k, r["Dispatch_Id"])
+            if key not in seen:
+                seen.add(key)
+                acc[k]["dispatch_ns@" + f.parent.name] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+                base = k.split("_")[-1] if k.startswith(("keying", "classify")) else None
+                if k.startswith("keying"):
+                    nbatch[base]["@" + f.parent.name] += 1
+                elif k in ("compare", "fill"):
+                    nbatch[k]["@" + f.parent.name] += 1
+
+    def batches(k, counter_file):
+        n = nbatch[k].get("@" + counter_file, 0)
+        return n if n else 1
+
+    summ = {}
+    for k, d in acc.items():
+        out = {}
+        for f in sorted(src.glob("pmc_*/run_counter_collection.csv")):
+            cols = {r["Counter_Name"] for r in csv.DictReader(open(f)) if kind(r["Kernel_Name"]) == k}
+            nb = batches(k, f.parent.name) if k in ("seal", "open", "compare", "fill") else 1
+            if k.startswith(("keying", "classify")):
+                nb = nbatch[k.split("_")[-1]].get("@" + f.parent.name, 1) or 1
+            for c in cols:
+                out[c] = d[c] / nb
+            if "dispatch_ns@" + f.parent.name in d:
+                out.setdefault("dispatch_ns", d["dispatch_ns@" + f.parent.name] / nb)
+        summ[k] = out
     (dst / f"{tag}_pmc_summary.json").write_text(json.dumps(summ, indent=1) + "\n")
     traffic = {"records": records, "record_bytes": record_bytes, "tag": tag,
                "method": "2*1024*FETCH_SIZE + 1024*WRITE_SIZE (gfx950 FETCH_SIZE half-count correction)"}
@@ -62,16 +96,27 @@ def main(tag: str, records: int = 1 << 20, record_bytes: int = 16384):
             traffic[f"{k}_write_bytes"] = wr
             traffic[f"{k}_bytes_per_launch"] = rd + wr
     if "compare_read_bytes" in traffic:
-        traffic["calibration"] = {"compare_expected_read": 2 * records * record_bytes,
+        traffic["calibration"] = {"compare_expected_read": 2 * records * record_bytes if record_bytes != "zipf"
+                                  else None,
                                   "compare_measured_read": traffic["compare_read_bytes"]}
     for k in ("seal", "open"):
         if k in summ and "GRBM_GUI_ACTIVE" in summ[k]:
             traffic[f"{k}_clock_ghz"] = summ[k]["GRBM_GUI_ACTIVE"] / 8 / summ[k]["dispatch_ns"]
         if k in summ and "SQ_INSTS_VALU" in summ[k]:
             traffic[f"{k}_valu_per_record"] = summ[k]["SQ_INSTS_VALU"] / records
+    try:
+        sys.path.insert(0, str(ROOT))
+        from suruga_amd import _native
+
+        traffic["kernels"] = _native.load().sg_build_info().decode()
+    except Exception:  # the summary is still useful without the build string
+        pass
     (dst / f"traffic_{tag}.json").write_text(json.dumps(traffic, indent=1) + "\n")
     print(json.dumps(traffic, indent=1))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "r01")
+    # pmc_traffic.py <tag> [records] [record_bytes|zipf]
+    a = sys.argv[1:]
+    rb = a[2] if len(a) > 2 else "16384"
+    main(a[0] if a else "r01", int(a[1]) if len(a) > 1 else 1 << 20, rb if rb == "zipf" else int(rb))

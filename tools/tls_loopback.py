@@ -56,54 +56,100 @@ def main():
             d[k] = d.get(k, 0.0) + x.value
 
     def writer():
+        # two stages: this thread seals chunk c+1 (sg_write_records, GIL
+        # released in the call) while a sender thread puts chunk c on the socket
+        import queue
+
         try:
             enc = ChaCha20Poly1305(args.device).new_encryptor(KEY_C2S)
             sock = socket.create_connection(("127.0.0.1", port))
             sock.setsockopt(socket.SOL_SOCKET, socket.SO_SNDBUF, 8 << 20)
-            wire = (C.c_uint8 * lib.sg_wire_bound(wchunk))()
+            nbuf = 3
+            wires = [(C.c_uint8 * lib.sg_wire_bound(wchunk))() for _ in range(nbuf)]
+            free, full = queue.Queue(), queue.Queue()
+            for w in range(nbuf):
+                free.put(w)
+            d = stats["writer"]
+            t_sock = [0.0]
+
+            def sender():
+                while True:
+                    item = full.get()
+                    if item is None:
+                        return
+                    w, ln = item
+                    t0 = time.perf_counter()
+                    sock.sendall(memoryview(wires[w])[:ln])
+                    t_sock[0] += time.perf_counter() - t0
+                    free.put(w)
+
+            th = threading.Thread(target=sender)
+            th.start()
             src = pattern.ctypes.data_as(C.c_void_p)
             wl = C.c_size_t(0)
-            seq, sent, t_sock = 0, 0, 0.0
-            d = stats["writer"]
+            seq, sent = 0, 0
             while sent < total:
                 n = min(wchunk, total - sent)
-                nrec = N.check(lib.sg_write_records(enc._ptr, seq, 23, 3, 3, src, n, wire, len(wire), C.byref(wl)))
+                w = free.get()
+                nrec = N.check(lib.sg_write_records(enc._ptr, seq, 23, 3, 3, src, n, wires[w], len(wires[w]),
+                                                    C.byref(wl)))
                 timing(d)
+                full.put((w, wl.value))
                 seq += nrec
-                t0 = time.perf_counter()
-                sock.sendall(memoryview(wire)[:wl.value])
-                t_sock += time.perf_counter() - t0
                 sent += n
+            full.put(None)
+            th.join()
             sock.shutdown(socket.SHUT_WR)
-            d["socket_ms"] = t_sock * 1e3
+            d["socket_ms"] = t_sock[0] * 1e3
             d["records"] = seq
         except Exception as e:  # pragma: no cover - reported below
             errors.append(("writer", repr(e)))
 
     def reader():
+        # two stages: a receiver thread fills 8 MiB blocks from the socket while
+        # this thread opens the complete records of the previous block
+        import queue
+
         try:
             dec = ChaCha20Poly1305(args.device).new_decryptor(KEY_C2S)
             conn, _ = srv.accept()
             conn.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 8 << 20)
-            cap = 64 << 20
+            blk = 8 << 20
+            blocks = queue.Queue(maxsize=4)
+            t_sock = [0.0]
+
+            def receiver():
+                while True:
+                    b = bytearray(blk)
+                    mv, have = memoryview(b), 0
+                    while have < blk:
+                        t0 = time.perf_counter()
+                        k = conn.recv_into(mv[have:], blk - have)
+                        t_sock[0] += time.perf_counter() - t0
+                        if k == 0:
+                            break
+                        have += k
+                    blocks.put((b, have))
+                    if have < blk:
+                        blocks.put(None)
+                        return
+
+            th = threading.Thread(target=receiver)
+            th.start()
+            cap = 2 * blk + (64 << 10)
             buf = bytearray(cap)
-            mv = memoryview(buf)
             have = 0
             out = np.empty(cap, dtype=np.uint8)
             res = N.SgReadResult()
-            seq, got, t_sock, mism, t_verify = 0, 0, 0.0, 0, 0.0
+            seq, got, mism, t_verify = 0, 0, 0, 0.0
             d = stats["reader"]
-            eof = False
-            while not eof:
-                t0 = time.perf_counter()
-                k = conn.recv_into(mv[have:], cap - have)
-                t_sock += time.perf_counter() - t0
-                eof = k == 0
-                have += k
-                if not eof and have < (8 << 20):
-                    continue  # batch up: one device round trip per few MiB
-                if have == 0:
+            while True:
+                item = blocks.get()
+                if item is None:
                     break
+                b, ln = item
+                buf[have:have + ln] = memoryview(b)[:ln]
+                have += ln
                 src = (C.c_uint8 * have).from_buffer(buf)
                 N.check(lib.sg_read_records(dec._ptr, seq, src, have, out.ctypes.data_as(C.c_void_p), cap,
                                             None, None, 1 << 20, C.byref(res)))
@@ -116,19 +162,21 @@ def main():
                 m, a = int(res.out_len), 0
                 while a < m:
                     off = (got + a) % wchunk
-                    ln = min(m - a, wchunk - off)
-                    if not np.array_equal(out[a:a + ln], pattern[off:off + ln]):
-                        mism += int(np.count_nonzero(out[a:a + ln] != pattern[off:off + ln]))
-                    a += ln
+                    ln2 = min(m - a, wchunk - off)
+                    if not np.array_equal(out[a:a + ln2], pattern[off:off + ln2]):
+                        mism += int(np.count_nonzero(out[a:a + ln2] != pattern[off:off + ln2]))
+                    a += ln2
                 got += m
                 t_verify += time.perf_counter() - t1
                 seq += res.records
                 c = int(res.consumed)
                 buf[:have - c] = buf[c:have]
                 have -= c
+            th.join()
             if have:
                 raise RuntimeError(f"{have} trailing bytes")
-            d.update(socket_ms=t_sock * 1e3, verify_ms=t_verify * 1e3, records=seq, bytes=got, mismatched_bytes=mism)
+            d.update(socket_ms=t_sock[0] * 1e3, verify_ms=t_verify * 1e3, records=seq, bytes=got,
+                     mismatched_bytes=mism)
         except Exception as e:  # pragma: no cover
             errors.append(("reader", repr(e)))
 
