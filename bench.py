@@ -252,7 +252,9 @@ def main():
             "higher_is_better": True, "scaling": "strong" if args.strong else "weak", "vs_baseline": None, "dtype": "u32",
             "data": "synthetic (splitmix64 records generated on device)",
             "config": dict(cfg, parallelism=f"record-shard x{world}", kernels=lib.sg_build_info().decode()),
-            "roofline": {"bound": "hbm", "kernel": f"sg_aead_kernel<{'OPEN' if dom == 'open' else 'SEAL'}>",
+            "roofline": {"bound": "hbm", "kernel": (f"sg_aead_kernel<{dom.upper()}, 256>" if args.workload == "c1" else
+                                                    f"sg_classify_kernel + sg_aead_list_kernel<{dom.upper()}, L=2..256> "
+                                                    "(one batch)"),
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "alg_bytes_per_launch": alg_bytes, "avg_launch_ms": round(dom_ms, 4)},

@@ -107,3 +107,33 @@ def test_no_cpu_fallback_in_product():
     for py in (ROOT / "suruga_amd").glob("*.py"):
         text = py.read_text()
         assert "import oracle" not in text and "oracle_ffi" not in text, py
+
+
+def test_record_header_parser_without_gpu(lib):
+    """sg_read_records checks headers (tls.rs:218-238) before any device work:
+    with no complete valid record in the buffer it returns the header error
+    without touching the context, so an opaque dummy handle suffices here."""
+    from suruga_amd._native import SG_E_RECORD_OVERFLOW, SG_E_SHORT, SG_E_UNEXPECTED_MESSAGE, SgReadResult
+
+    dummy = C.create_string_buffer(64)  # never dereferenced on these paths
+    res = SgReadResult()
+
+    def parse(wire: bytes):
+        buf = C.create_string_buffer(wire, len(wire))
+        out = C.create_string_buffer(max(len(wire), 1))
+        assert lib.sg_read_records(C.cast(dummy, C.c_void_p), 0, buf, len(wire), out, len(out), None, None, 16,
+                                   C.byref(res)) == 0
+        return res.error, res.records, res.consumed
+
+    assert parse(bytes([0x18, 3, 3, 0, 3, 1, 2, 3])) == (SG_E_UNEXPECTED_MESSAGE, 0, 0)  # tls.rs:427-436
+    n = 16384 + 2048 + 1
+    assert parse(bytes([23, 3, 3, n >> 8, n & 0xFF])) == (SG_E_RECORD_OVERFLOW, 0, 0)   # tls.rs:232-234
+    assert parse(bytes([23, 3, 3, 0, 15]) + bytes(15)) == (SG_E_SHORT, 0, 0)             # < mac_len
+    n = 16384 + 17
+    assert parse(bytes([23, 3, 3, n >> 8, n & 0xFF]) + bytes(n)) == (SG_E_RECORD_OVERFLOW, 0, 0)
+    assert parse(bytes([23, 3, 3, 0, 40]) + bytes(10)) == (0, 0, 0)   # incomplete: wait for more bytes
+    assert parse(bytes([23, 3])) == (0, 0, 0)
+    assert lib.sg_wire_bound(0) == 0
+    assert lib.sg_wire_bound(1) == 1 + 21
+    assert lib.sg_wire_bound(16384) == 16384 + 21
+    assert lib.sg_wire_bound(16385) == 16385 + 42
