@@ -141,7 +141,11 @@ typedef struct sg_batch {
     uint8_t*        status;
 
     /* HIP stream (hipStream_t) or NULL for the library's per-device stream.
-     * The call is asynchronous on that stream when `stream` is non-NULL.    */
+     * The call is asynchronous on that stream when `stream` is non-NULL,
+     * except that a mixed-size batch (len != NULL, records in more than one
+     * size class) waits once for its classification so that every class runs
+     * on an exact grid.  Under stream capture it does not wait (persistent
+     * class grids), so the whole call is graph-capturable with a workspace. */
     void*           stream;
 
     /* scratch of >= sg_workspace_size(count) bytes of device memory, or NULL

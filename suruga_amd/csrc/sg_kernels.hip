@@ -666,21 +666,28 @@ __global__ __launch_bounds__(256) void sg_aead_kernel(const KParams p) {
     aead_record<OPEN, L>(p, rec, rec < p.count, lds + g * p.lds_rec_bytes, t);
 }
 
-// Bucketed launch: records listed by sg_classify_kernel for this size class;
-// a fixed grid walks the list (the class population is only known on device).
-template <bool OPEN, uint32_t L>
+// Bucketed launch: records listed by sg_classify_kernel for this size class.
+// PERSIST = false: the host read the class population back and sized the grid
+// exactly (one record group per workgroup, like the direct kernel: waves that
+// finish their ChaCha20 share exit and free their slots while wave 0 runs the
+// MAC).  PERSIST = true (stream capture, where the host cannot wait): a fixed
+// grid walks the list; the barrier closing each iteration makes waves 1-3
+// wait for wave 0's MAC, ~30 % slower per byte (tools/exp_list.py).
+template <bool OPEN, uint32_t L, bool PERSIST>
 __global__ __launch_bounds__(256) void sg_aead_list_kernel(const KParams p, const uint32_t* __restrict__ list,
                                                            const uint32_t* __restrict__ list_count) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     constexpr uint32_t RPW = 256u / L;
     const uint32_t g = group_of_thread<L>(), t = threadIdx.x % L;
     const uint32_t cnt = *list_count;
-    for (uint32_t base = blockIdx.x * RPW; base < cnt; base += gridDim.x * RPW) {
+    const uint32_t stride = PERSIST ? gridDim.x * RPW : 0xffffffffu;
+    for (uint32_t base = blockIdx.x * RPW; base < cnt; base += stride) {
         const uint32_t slot = base + g;
         const bool active = slot < cnt;
         uint32_t rec = active ? list[slot] : 0u;
         if constexpr (L >= 64u) rec = __builtin_amdgcn_readfirstlane(rec);
         aead_record<OPEN, L>(p, rec, active, lds + g * p.lds_rec_bytes, t);
+        if constexpr (!PERSIST) break;
         __syncthreads();  // LDS is reused by the next iteration
     }
 }
@@ -814,27 +821,37 @@ hipError_t launch_direct(const KParams& p, hipStream_t s) {
     return hipGetLastError();
 }
 
+// n_exact: the class population when the host knows it (exact grid), or
+// UINT32_MAX for a persistent grid capped at kListGridPerCU workgroups per CU.
 template <bool OPEN, uint32_t L>
-hipError_t launch_list(const KParams& p, const uint32_t* list, const uint32_t* cnt, hipStream_t s) {
+hipError_t launch_list(const KParams& p, const uint32_t* list, const uint32_t* cnt, uint32_t n_exact,
+                       hipStream_t s) {
     constexpr uint32_t RPW = 256u / L;
+    const size_t lds = RPW * p.lds_rec_bytes;
+    if (n_exact != 0xffffffffu) {
+        if (n_exact == 0) return hipSuccess;
+        hipLaunchKernelGGL((sg_aead_list_kernel<OPEN, L, false>), dim3((n_exact + RPW - 1u) / RPW), dim3(kThreads),
+                           lds, s, p, list, cnt);
+        return hipGetLastError();
+    }
     uint32_t grid = (p.count + RPW - 1u) / RPW;
     const uint32_t cap = kListGridPerCU * 256u;
     if (grid > cap) grid = cap;
-    hipLaunchKernelGGL((sg_aead_list_kernel<OPEN, L>), dim3(grid), dim3(kThreads), RPW * p.lds_rec_bytes, s, p,
-                       list, cnt);
+    hipLaunchKernelGGL((sg_aead_list_kernel<OPEN, L, true>), dim3(grid), dim3(kThreads), lds, s, p, list, cnt);
     return hipGetLastError();
 }
 
 template <bool OPEN>
-hipError_t launch_class(uint32_t c, const KParams& q, const uint32_t* list, const uint32_t* cnt, hipStream_t s) {
+hipError_t launch_class(uint32_t c, const KParams& q, const uint32_t* list, const uint32_t* cnt, uint32_t n_exact,
+                        hipStream_t s) {
 #define SG_CLASS_CASE(C)                                                                  \
     case C:                                                                               \
-        return list ? launch_list<OPEN, class_lanes(C)>(q, list, cnt, s)                  \
+        return list ? launch_list<OPEN, class_lanes(C)>(q, list, cnt, n_exact, s)         \
                     : launch_direct<OPEN, class_lanes(C)>(q, s);
     switch (c) {
         SG_CLASS_CASE(0) SG_CLASS_CASE(1) SG_CLASS_CASE(2) SG_CLASS_CASE(3)
         SG_CLASS_CASE(4) SG_CLASS_CASE(5) SG_CLASS_CASE(6)
-        default: return list ? launch_list<OPEN, class_lanes(7)>(q, list, cnt, s)
+        default: return list ? launch_list<OPEN, class_lanes(7)>(q, list, cnt, n_exact, s)
                              : launch_direct<OPEN, class_lanes(7)>(q, s);
     }
 #undef SG_CLASS_CASE
@@ -847,7 +864,7 @@ hipError_t launch_aead_t(const KParams& p, uint32_t max_n, bool uniform, uint32_
         KParams q = p;
         const uint32_t c = size_class(max_n);
         q.lds_rec_bytes = lds_rec_bytes(c, q.ad_len, max_n);
-        return launch_class<OPEN>(c, q, nullptr, nullptr, s);
+        return launch_class<OPEN>(c, q, nullptr, nullptr, 0, s);
     }
     hipError_t e = hipMemsetAsync(counts, 0, kNumClasses * sizeof(uint32_t), s);
     if (e != hipSuccess) return e;
@@ -855,12 +872,24 @@ hipError_t launch_aead_t(const KParams& p, uint32_t max_n, bool uniform, uint32_
     hipLaunchKernelGGL(sg_classify_kernel<OPEN>, dim3((p.count + per_wg - 1u) / per_wg), dim3(kClassifyThreads), 0, s,
                        p, lists, counts);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    // one launch per possibly populated class, largest records first
+    // Read the class populations back (one stream sync per mixed batch) so every
+    // class runs on an exact grid; under stream capture the host cannot wait,
+    // so the classes run on persistent grids instead.
+    uint32_t pop[kNumClasses];
+    hipStreamCaptureStatus cap_status = hipStreamCaptureStatusNone;
+    if ((e = hipStreamIsCapturing(s, &cap_status)) != hipSuccess) return e;
+    const bool exact = cap_status == hipStreamCaptureStatusNone;
+    if (exact) {
+        if ((e = hipMemcpyAsync(pop, counts, sizeof pop, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+        if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+    }
+    // one launch per populated class, largest records first
     KParams q = p;
     for (int c = (int)size_class(max_n); c >= 0; --c) {
         const uint32_t cap = max_n < class_max((uint32_t)c) ? max_n : class_max((uint32_t)c);
         q.lds_rec_bytes = lds_rec_bytes((uint32_t)c, q.ad_len, cap);
-        if ((e = launch_class<OPEN>((uint32_t)c, q, lists + (uint64_t)c * p.count, counts + c, s)) != hipSuccess)
+        if ((e = launch_class<OPEN>((uint32_t)c, q, lists + (uint64_t)c * p.count, counts + c,
+                                    exact ? pop[c] : 0xffffffffu, s)) != hipSuccess)
             return e;
     }
     return hipSuccess;
@@ -893,8 +922,8 @@ hipError_t launch_compare(const uint8_t* a, uint64_t sa, const uint8_t* b, uint6
 const char* kernel_config() {
 #define SG_STR2(x) #x
 #define SG_STR(x) SG_STR2(x)
-    return "gfx950 sg_aead_kernel v6" "/salu_pre=" SG_STR(SG_SALU_PRE)
-           ": 8 size classes (2..256 lanes per record, one 64-B block per lane, device bucketing), "
+    return "gfx950 sg_aead_kernel v7" "/salu_pre=" SG_STR(SG_SALU_PRE)
+           ": 8 size classes (2..256 lanes per record, one 64-B block per lane, device bucketing, exact class grids), "
            "lane=64B ChaCha block (counter-free round-1 QRs on SALU for wave-uniform records), Poly1305 contiguous-chunk Horner radix-2^32 (clamped r) on min(L,64) lanes + "
            "per-lane r^(k(PL-1-t)) scale + shuffle sum, keying pre-pass";
 }

@@ -313,3 +313,40 @@ def test_c2_zipf_sample_bit_exact(gpu, oracle):
                     out_off=t64(lay.in_off), status=st, **common))
     torch.cuda.synchronize()
     assert host(st) == bytes(count) and host(back) == pt_h
+
+
+def test_mixed_batch_graph_capture(gpu, oracle):
+    """A mixed-size batch captured into a HIP graph (the library then uses
+    persistent class grids instead of reading the class populations back) and
+    replayed: same bytes as the oracle."""
+    torch = torch_mod()
+    from suruga_amd import batch as B
+    from suruga_amd import workloads as W
+
+    count = 1500
+    lay = W.c2_layout(count)
+    rng = np.random.default_rng(17)
+    pt_h = rng.bytes(lay.pt_bytes)
+    t64 = lambda a: torch.from_numpy(a.view(np.int64)).to("cuda")
+    t32 = lambda a: torch.from_numpy(a.view(np.int32)).to("cuda")
+    keys = dev_bytes(lay.keys).view(-1, 32)
+    pt = dev_bytes(pt_h)
+    ct = torch.zeros(lay.ct_bytes, dtype=torch.uint8, device="cuda")
+    ws = torch.empty(B.workspace_size(count), dtype=torch.uint8, device="cuda")
+    lens, in_off, out_off = t32(lay.lens), t64(lay.in_off), t64(lay.out_off)
+    kidx, seq = t32(lay.key_index), t64(lay.seq)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        b = B.Batch(count=count, keys=keys, inp=pt, out=ct, lens=lens, max_len=int(lay.lens.max()), in_off=in_off,
+                    out_off=out_off, key_index=kidx, seq=seq, workspace=ws, stream=torch.cuda.current_stream())
+        B.seal(b)
+    ct.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    ct_h = host(ct)
+    for i in range(0, count, 7):
+        k = lay.keys[32 * lay.key_index[i]:32 * lay.key_index[i] + 32]
+        s, n, o, q = int(lay.seq[i]), int(lay.lens[i]), int(lay.in_off[i]), int(lay.out_off[i])
+        exp = oracle.seal(k, struct.pack(">Q", s), pt_h[o:o + n], oracle.tls_ad(s, n))
+        assert ct_h[q:q + n + 16] == exp, (i, n)
