@@ -90,9 +90,27 @@ def build_cpp_tests(force: bool = False) -> Path:
     return CPP_TEST_BIN
 
 
+OSSL_SRC = ORACLE_DIR / "ossl_aead.c"
+OSSL_LIB = ORACLE_DIR / "libossl_aead.so"
+
+
+def build_ossl(force: bool = False):
+    """The OpenSSL-composed CPU comparison line (bench only).  Optional: None
+    when libcrypto headers are absent."""
+    if not Path("/usr/include/openssl/evp.h").exists():
+        return OSSL_LIB if OSSL_LIB.exists() else None
+    if force or _stale(OSSL_LIB, [OSSL_SRC]):
+        tmp = OSSL_LIB.with_suffix(".so.tmp")
+        _run(["gcc", "-O2", "-std=c11", "-Wall", "-fPIC", "-shared", "-pthread", "-o", str(tmp), str(OSSL_SRC),
+              "-lcrypto"])
+        os.replace(tmp, OSSL_LIB)
+    return OSSL_LIB
+
+
 def build_all(force: bool = False) -> None:
     build_library(force)
     build_oracle(force)
+    build_ossl(force)
     build_cpp_tests(force)
 
 

@@ -163,3 +163,24 @@ def test_fill_record_rule(oracle):
     for i in range(20):
         w = oracle.L.so_splitmix64(seed ^ (j << 32) ^ (i // 8))
         assert buf[i] == (w >> (8 * (i % 8))) & 0xFF
+
+
+def test_openssl_comparison_line_matches_oracle(oracle):
+    """bench.py's optimised-CPU line must compute suruga's AEAD, not RFC 7539."""
+    from oracle_ffi import OsslLine
+
+    try:
+        ossl = OsslLine()
+    except OSError as e:
+        pytest.skip(str(e))
+    key = bytes(range(32))
+    for n, count in ((0, 3), (1, 5), (64, 4), (1000, 7), (16384, 3)):
+        pt = b"".join(oracle.fill_record(7, j, n) for j in range(count))
+        ct = ossl.seal_batch_tls(key, 0xFFFFFFFE, pt, n, count, threads=2)
+        assert ct == oracle.seal_batch_tls(key, 0xFFFFFFFE, pt, n, count)
+        bad, back = ossl.open_batch_tls(key, 0xFFFFFFFE, ct, n, count, threads=2)
+        assert bad == 0 and back == pt
+        if count:
+            t = bytearray(ct)
+            t[-1] ^= 1
+            assert ossl.open_batch_tls(key, 0xFFFFFFFE, bytes(t), n, count)[0] == 1
