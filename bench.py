@@ -54,29 +54,49 @@ def parse():
 
 
 def cpu_baseline(args, n):
-    """Oracle (suruga-algorithm C restatement) on the host cores: bounded sample."""
+    """CPU lines on the host cores, bounded samples; only the C calls are timed
+    (buffers preallocated).  kind "port": the oracle (the reference's scalar
+    algorithm restated in C); optimised_cpu: the same AEAD composed from
+    OpenSSL's vectorised ChaCha20 / Poly1305 (SURVEY.md 8d's optional line)."""
+    import ctypes as C
+
+    import numpy as np
+
     sys.path.insert(0, str(ROOT / "tests"))
-    from oracle_ffi import oracle as get_oracle  # checker/baseline only, never the measured path
+    from oracle_ffi import OsslLine  # checker/baseline only, never the measured path
+    from oracle_ffi import oracle as get_oracle
 
     o = get_oracle()
     count = args.cpu_sample
     threads = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()))
-    pt = b"".join(o.fill_record(SEED, j, n) for j in range(count))
-    reps, t = 0, 0.0
-    while t < args.cpu_seconds:
-        t0 = time.perf_counter()
-        ct = o.seal_batch_tls(KEY, 0, pt, n, count, threads=threads)
-        bad, back, _ = o.open_batch_tls(KEY, 0, ct, n, count, threads=threads)
-        t += time.perf_counter() - t0
-        reps += 1
-        assert bad == 0 and back == pt
-    gibs = 2 * count * n * reps / t / 2**30
-    # single-thread rate on a slice (the reference is single-threaded per connection)
-    c1 = max(64, count // 16)
-    t0 = time.perf_counter()
-    ct1 = o.seal_batch_tls(KEY, 0, pt[:c1 * n], n, c1, threads=1)
-    o.open_batch_tls(KEY, 0, ct1, n, c1, threads=1)
-    t1 = time.perf_counter() - t0
+    pt = np.empty(count * n, dtype=np.uint8)
+    ct = np.empty(count * (n + 16), dtype=np.uint8)
+    back = np.empty(count * n, dtype=np.uint8)
+    st = np.empty(count, dtype=np.uint8)
+    ptr = lambda a, off=0: C.c_void_p(a.ctypes.data + off)  # noqa: E731
+    for j in range(count):
+        o.L.so_fill_record(SEED, j, ptr(pt, j * n), n)
+
+    def timed(seal, open_, recs, thr):
+        reps, t = 0, 0.0
+        while t < args.cpu_seconds or reps == 0:
+            t0 = time.perf_counter()
+            seal(recs, thr)
+            bad = open_(recs, thr)
+            t += time.perf_counter() - t0
+            reps += 1
+            assert bad == 0
+        assert np.array_equal(back[:recs * n], pt[:recs * n])
+        return 2 * recs * n * reps / t / 2**30, reps
+
+    def o_seal(recs, thr):
+        o.L.so_seal_batch_tls(KEY, 0, ptr(pt), n, recs, ptr(ct), thr)
+
+    def o_open(recs, thr):
+        return o.L.so_open_batch_tls(KEY, 0, ptr(ct), n, recs, ptr(back), ptr(st), thr)
+
+    gibs, reps = timed(o_seal, o_open, count, threads)
+    one, _ = timed(o_seal, o_open, max(64, count // 16), 1)  # the reference is single-threaded per connection
     model = ""
     try:
         for line in open("/proc/cpuinfo"):
@@ -85,31 +105,28 @@ def cpu_baseline(args, n):
                 break
     except OSError:
         pass
-    # optimised-CPU comparison line: the same AEAD composed from
-    # OpenSSL's vectorised ChaCha20 and Poly1305 (oracle/ossl_aead.c)
-    ossl = None
     try:
-        from oracle_ffi import OsslLine
+        L = OsslLine().L
 
-        line = OsslLine()
-        r2, t2 = 0, 0.0
-        while t2 < args.cpu_seconds:
-            t0 = time.perf_counter()
-            ct2 = line.seal_batch_tls(KEY, 0, pt, n, count, threads=threads)
-            bad2, _ = line.open_batch_tls(KEY, 0, ct2, n, count, threads=threads)
-            t2 += time.perf_counter() - t0
-            r2 += 1
-            assert bad2 == 0
-        ossl = {"value": round(2 * count * n * r2 / t2 / 2**30, 3), "unit": "GiB/s", "cores": threads,
-                "impl": "OpenSSL libcrypto EVP_chacha20 + EVP_MAC POLY1305 composed per suruga's AEAD",
-                "sample": f"{count} x {n} B TLS records seal+open, x{r2} repetitions"}
+        def s_seal(recs, thr):
+            L.ossl_batch_tls(0, KEY, 0, ptr(pt), n, recs, ptr(ct), thr)
+
+        def s_open(recs, thr):
+            return L.ossl_batch_tls(1, KEY, 0, ptr(ct), n, recs, ptr(back), thr)
+
+        og, oreps = timed(s_seal, s_open, count, threads)
+        o1, _ = timed(s_seal, s_open, max(64, count // 16), 1)
+        ossl = {"value": round(og, 3), "unit": "GiB/s", "cores": threads, "single_thread_gibs": round(o1, 4),
+                "impl": "OpenSSL libcrypto EVP_chacha20 + EVP_MAC POLY1305 composed per suruga's AEAD "
+                        "(oracle/ossl_aead.c)",
+                "sample": f"{count} x {n} B TLS records seal+open, x{oreps} repetitions"}
     except (OSError, AssertionError) as e:
         ossl = {"unavailable": str(e)}
     return {
         "value": round(gibs, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
         "sample": f"{count} x {n} B TLS records seal+open, x{reps} repetitions, {threads} threads "
                   f"(oracle/suruga_oracle.c, the reference's scalar algorithm)",
-        "single_thread_gibs": round(2 * c1 * n / t1 / 2**30, 4), "cpu": model or platform.processor(),
+        "single_thread_gibs": round(one, 4), "cpu": model or platform.processor(),
         "optimised_cpu": ossl,
     }
 

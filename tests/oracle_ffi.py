@@ -143,17 +143,17 @@ class OsslLine:
             raise OSError("libossl_aead.so unavailable (no libcrypto headers)")
         self.L = C.CDLL(str(path))
         self.L.ossl_batch_tls.restype = C.c_size_t
-        self.L.ossl_batch_tls.argtypes = [C.c_int, C.c_char_p, C.c_uint64, C.c_char_p, C.c_size_t, C.c_size_t,
+        self.L.ossl_batch_tls.argtypes = [C.c_int, C.c_char_p, C.c_uint64, C.c_void_p, C.c_size_t, C.c_size_t,
                                           C.c_void_p, C.c_int]
 
     def seal_batch_tls(self, key, seq0, pt, n, count, threads=1) -> bytes:
         out = C.create_string_buffer((n + 16) * count)
-        rc = self.L.ossl_batch_tls(0, key, seq0, pt, n, count, out, threads)
+        rc = self.L.ossl_batch_tls(0, key, seq0, C.cast(C.c_char_p(pt), C.c_void_p), n, count, out, threads)
         if rc == C.c_size_t(-1).value:
             raise OSError("POLY1305 not available in libcrypto")
         return out.raw
 
     def open_batch_tls(self, key, seq0, ct, n, count, threads=1):
         out = C.create_string_buffer(max(n * count, 1))
-        bad = self.L.ossl_batch_tls(1, key, seq0, ct, n, count, out, threads)
+        bad = self.L.ossl_batch_tls(1, key, seq0, C.cast(C.c_char_p(ct), C.c_void_p), n, count, out, threads)
         return bad, out.raw[:n * count]
