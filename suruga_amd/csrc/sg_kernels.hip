@@ -549,6 +549,21 @@ __device__ __forceinline__ void aead_record(const KParams& p, const uint32_t rec
     if (!work || t >= PL) return;
 
     // ---- phase 2: Poly1305 on PL lanes -----------------------------------------
+    // open: lane 0 fetches the received tag now so that its memory latency
+    // hides behind the Horner loop instead of stalling the final compare
+    uint32_t rx[4] = {0u, 0u, 0u, 0u};
+    if constexpr (OPEN) {
+        if (t == 0) {
+            const uint8_t* ep = in + n;
+            if ((((uintptr_t)ep) & 3u) == 0u) {
+                const uint32_t* e32 = reinterpret_cast<const uint32_t*>(ep);
+                rx[0] = e32[0]; rx[1] = e32[1]; rx[2] = e32[2]; rx[3] = e32[3];
+            } else {
+#pragma unroll
+                for (int i = 0; i < 16; ++i) rx[i >> 2] |= (uint32_t)ep[i] << (8 * (i & 3));
+            }
+        }
+    }
     const MacGeom g = mac_geom(adlen, n, PL);
     const uint32_t* kr = p.ws + (uint64_t)rec * kKeyRecWords;
     uint32_t r0 = kr[kR32Off + 0], r1 = kr[kR32Off + 1], r2 = kr[kR32Off + 2], r3 = kr[kR32Off + 3];
@@ -637,10 +652,7 @@ __device__ __forceinline__ void aead_record(const KParams& p, const uint32_t rec
         }
     } else {
         // constant-time compare: diff |= a ^ b over all 16 bytes (:84-87)
-        const uint8_t* ep = in + n;
-        uint32_t diff = 0;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) diff |= (uint32_t)(ep[i] ^ (uint8_t)(tw[i >> 2] >> (8 * (i & 3))));
+        const uint32_t diff = (rx[0] ^ tw[0]) | (rx[1] ^ tw[1]) | (rx[2] ^ tw[2]) | (rx[3] ^ tw[3]);
         p.status[rec] = diff != 0u ? 1u : 0u;
     }
 }
