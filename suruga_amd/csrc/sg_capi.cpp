@@ -248,13 +248,13 @@ sg_ctx* sg_ctx_new(const uint8_t key[32], int device) {
     }
     sg_ctx* c = new sg_ctx();
     c->device = device;
-    const size_t cap = SG_MAX_RECORD_LEN + 64;
+    const size_t cap_in = sg::kSingleInOff + SG_MAX_RECORD_LEN + 64;
+    const size_t cap_out = sg::kSingleOutOff + SG_MAX_RECORD_LEN + 64;
     bool ok = hipMalloc((void**)&c->d_key, 64) == hipSuccess &&
-              hipMalloc((void**)&c->d_nonce, 64) == hipSuccess &&
-              hipMalloc((void**)&c->d_ad, 512) == hipSuccess &&
-              hipMalloc((void**)&c->d_in, cap) == hipSuccess &&
-              hipMalloc((void**)&c->d_out, cap) == hipSuccess &&
-              hipMalloc((void**)&c->d_status, 64) == hipSuccess &&
+              hipMalloc((void**)&c->d_in, cap_in) == hipSuccess &&
+              hipMalloc((void**)&c->d_out, cap_out) == hipSuccess &&
+              hipHostMalloc((void**)&c->h_in, cap_in, hipHostMallocDefault) == hipSuccess &&
+              hipHostMalloc((void**)&c->h_out, cap_out, hipHostMallocDefault) == hipSuccess &&
               hipMalloc(&c->d_ws, sg_workspace_size(1)) == hipSuccess &&
               hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
               hipMemcpy(c->d_key, key, 32, hipMemcpyHostToDevice) == hipSuccess;
@@ -272,11 +272,10 @@ void sg_ctx_free(sg_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     sg::record_staging_free(c->rec);
     (void)hipFree(c->d_key);
-    (void)hipFree(c->d_nonce);
-    (void)hipFree(c->d_ad);
     (void)hipFree(c->d_in);
     (void)hipFree(c->d_out);
-    (void)hipFree(c->d_status);
+    (void)hipHostFree(c->h_in);
+    (void)hipHostFree(c->h_out);
     (void)hipFree(c->d_ws);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -295,39 +294,42 @@ static int single(sg_ctx* c, bool open, const uint8_t* nonce, size_t nonce_len, 
 
     std::lock_guard<std::mutex> lk(c->mu);
     SG_HIP(hipSetDevice(c->device));
-    SG_HIP(hipMemcpyAsync(c->d_nonce, nonce, 8, hipMemcpyHostToDevice, c->stream));
-    if (adlen) SG_HIP(hipMemcpyAsync(c->d_ad, ad, adlen, hipMemcpyHostToDevice, c->stream));
-    if (in_len) SG_HIP(hipMemcpyAsync(c->d_in, in, in_len, hipMemcpyHostToDevice, c->stream));
+    // one H2D copy of nonce | ad | record through the pinned block
+    std::memcpy(c->h_in, nonce, 8);
+    if (adlen) std::memcpy(c->h_in + sg::kSingleAdOff, ad, adlen);
+    if (in_len) std::memcpy(c->h_in + sg::kSingleInOff, in, in_len);
+    SG_HIP(hipMemcpyAsync(c->d_in, c->h_in, sg::kSingleInOff + in_len, hipMemcpyHostToDevice, c->stream));
 
     sg_batch b;
     std::memset(&b, 0, sizeof b);
     b.count = 1;
     b.keys = c->d_key;
     b.num_keys = 1;
-    b.nonces = c->d_nonce;
-    b.ads = c->d_ad;
+    b.nonces = c->d_in;
+    b.ads = c->d_in + sg::kSingleAdOff;
     b.ad_len = (uint32_t)adlen;
     b.ad_stride = (uint32_t)adlen;
-    b.in = c->d_in;
+    b.in = c->d_in + sg::kSingleInOff;
     b.in_stride = in_len;
-    b.out = c->d_out;
+    b.out = c->d_out + sg::kSingleOutOff;
     b.out_stride = in_len + 16;
     b.uniform_len = (uint32_t)in_len;
-    b.status = c->d_status;
+    b.status = c->d_out;
     b.stream = c->stream;
     b.workspace = c->d_ws;
     b.workspace_size = sg_workspace_size(1);
     int rc = open ? sg_open_batch(&b) : sg_seal_batch(&b);
     if (rc != SG_OK) return rc;
+    // one D2H copy of status | output
     const size_t out_len = open ? n : n + SG_MAC_LEN;
-    uint8_t st = 0;
-    if (out_len) SG_HIP(hipMemcpyAsync(out, c->d_out, out_len, hipMemcpyDeviceToHost, c->stream));
-    if (open) SG_HIP(hipMemcpyAsync(&st, c->d_status, 1, hipMemcpyDeviceToHost, c->stream));
+    SG_HIP(hipMemcpyAsync(c->h_out, c->d_out, sg::kSingleOutOff + out_len, hipMemcpyDeviceToHost, c->stream));
     SG_HIP(hipStreamSynchronize(c->stream));
+    const uint8_t st = open ? c->h_out[0] : 0;
     if (open && st != 0) {
         if (n) std::memset(out, 0, n);  // the reference releases no plaintext with Err
         return st == 2 ? SG_E_SHORT : SG_E_BAD_MAC;
     }
+    if (out_len) std::memcpy(out, c->h_out + sg::kSingleOutOff, out_len);
     return SG_OK;
 }
 

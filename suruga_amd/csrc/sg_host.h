@@ -28,14 +28,23 @@ void record_staging_free(RecordStaging* rs);
 // One context per direction (Aead::new_encryptor / new_decryptor): the key on
 // the device, staging for single records, and (lazily) the record-layer
 // pipeline of sg_write_records / sg_read_records.
+// Single-record staging (sg_seal / sg_open): one pinned host block and one
+// device block per direction, so a call is one H2D copy, the keying and AEAD
+// launches, and one D2H copy:
+//   in  block: nonce @0 | ad @kSingleAdOff | record @kSingleInOff
+//   out block: status @0 | output @kSingleOutOff
+namespace sg {
+constexpr size_t kSingleAdOff = 16;
+constexpr size_t kSingleInOff = 512;
+constexpr size_t kSingleOutOff = 64;
+}  // namespace sg
 struct sg_ctx {
     int device = 0;
     uint8_t* d_key = nullptr;      // 32 B
-    uint8_t* d_nonce = nullptr;    // 8 B
-    uint8_t* d_ad = nullptr;       // SG_MAX_AD_LEN
-    uint8_t* d_in = nullptr;       // SG_MAX_RECORD_LEN + 16
-    uint8_t* d_out = nullptr;      // SG_MAX_RECORD_LEN + 16
-    uint8_t* d_status = nullptr;   // 1
+    uint8_t* d_in = nullptr;       // kSingleInOff + SG_MAX_RECORD_LEN + 64
+    uint8_t* d_out = nullptr;      // kSingleOutOff + SG_MAX_RECORD_LEN + 64
+    uint8_t* h_in = nullptr;       // pinned mirrors of the two blocks
+    uint8_t* h_out = nullptr;
     void* d_ws = nullptr;
     hipStream_t stream = nullptr;
     sg::RecordStaging* rec = nullptr;
