@@ -183,11 +183,13 @@ int64_t sg_write_records(sg_ctx* c, uint64_t seq0, uint8_t content_type, uint8_t
         if (next < nrec) {
             const uint32_t k = (uint32_t)std::min<uint64_t>(kChunk, nrec - next);
             const double t0 = now_ms();
+            bool same = true;  // every record of the chunk has the same length
             for (uint32_t i = 0; i < k; ++i) {
                 const uint64_t r = next + i;
                 const uint32_t n = (uint32_t)std::min<uint64_t>(SG_RECORD_MAX_LEN, len - r * SG_RECORD_MAX_LEN);
                 std::memcpy(s.h_in + (size_t)i * kSlot, data + r * SG_RECORD_MAX_LEN, n);
                 s.h_len[i] = n;
+                same = same && n == s.h_len[0];
             }
             t_host += now_ms() - t0;
             SG_HIP(hipEventRecord(s.ev[0], s.st));
@@ -208,7 +210,9 @@ int64_t sg_write_records(sg_ctx* c, uint64_t seq0, uint8_t content_type, uint8_t
             b.in_stride = kSlot;
             b.out = s.d_out;
             b.out_stride = kSlot;
-            b.len = s.d_len;
+            // a uniform chunk is a direct launch; a ragged one (the tail) is bucketed
+            b.len = same ? nullptr : s.d_len;
+            b.uniform_len = same ? s.h_len[0] : 0u;
             b.max_len = SG_RECORD_MAX_LEN;
             b.stream = s.st;
             b.workspace = s.d_ws;
@@ -314,8 +318,10 @@ int sg_read_records(sg_ctx* c, uint64_t seq0, const uint8_t* wire, size_t wire_l
         if (next < nrec && error == SG_OK) {
             const uint32_t k = (uint32_t)std::min<uint64_t>(kChunk, nrec - next);
             const double t0 = now_ms();
+            bool same = true;
             for (uint32_t i = 0; i < k; ++i) {
                 const Rec& R = recs[next + i];
+                same = same && R.flen == recs[next].flen;
                 const uint64_t seq = seq0 + next + i;
                 std::memcpy(s.h_in + (size_t)i * kSlot, wire + R.off, R.flen);
                 s.h_len[i] = R.flen;
@@ -350,7 +356,8 @@ int sg_read_records(sg_ctx* c, uint64_t seq0, const uint8_t* wire, size_t wire_l
             b.in_stride = kSlot;
             b.out = s.d_out;
             b.out_stride = kSlot;
-            b.len = s.d_len;
+            b.len = same ? nullptr : s.d_len;
+            b.uniform_len = same ? recs[next].flen : 0u;
             b.max_len = SG_ENC_RECORD_MAX_LEN;
             b.status = s.d_status;
             b.stream = s.st;
