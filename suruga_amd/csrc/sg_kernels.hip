@@ -33,6 +33,9 @@
 #ifndef SG_SALU_PRE
 #define SG_SALU_PRE 1  // hoist the counter-free part of ChaCha round 1 to the SALU
 #endif
+#ifndef SG_MAC_V2
+#define SG_MAC_V2 1  // MAC loop: unaligned 16-byte LDS block loads, pad bit folded (see aead_record)
+#endif
 
 namespace sg {
 namespace {
@@ -51,6 +54,9 @@ __device__ __forceinline__ u32x4 ld16(const void* p) {
 __device__ __forceinline__ void st16(void* p, u32x4 v) {
     *reinterpret_cast<u32x4*>(__builtin_assume_aligned(p, 16)) = v;
 }
+// 16 bytes at any byte address (LDS: one ds_read_b128 on gfx950)
+typedef u32x4 u32x4_u __attribute__((aligned(1)));
+__device__ __forceinline__ u32x4 ldu16(const void* p) { return *reinterpret_cast<const u32x4_u*>(p); }
 
 // chacha20.rs:63-81
 #define SG_QR(a, b, c, d)                   \
@@ -573,12 +579,65 @@ __device__ __forceinline__ void aead_record(const KParams& p, const uint32_t rec
     const uint32_t s1 = r1 + (r1 >> 2), s2 = r2 + (r2 >> 2), s3 = r3 + (r3 >> 2);
 
     // lane t: virtual blocks [t*k, t*k + k); virtual block v is real iff v >= z
-    const uint32_t sh = (S & 3u) * 8u;
     const uint32_t v0 = t * g.k;
-    uint32_t pos = S - 16u * g.z + 16u * v0;
-    const uint32_t* l32 = reinterpret_cast<const uint32_t*>(lds);
     const uint32_t rem = g.L - 16u * (g.B - 1u);  // bytes in the final block, 1..16
     H32 h = {0u, 0u, 0u, 0u, 0u};
+#if SG_MAC_V2
+    // Every block is stepped with the 2^128 pad bit; the virtual blocks (the
+    // first z of the record, all in lanes t <= tp = z / k) are then discarded
+    // instead of being masked block by block: lanes t < tp hold only virtual
+    // blocks and drop their sum at the end, lane tp restarts from h = 0 after
+    // its first nv = z mod k blocks.  Dropping a prefix of a Horner chain is
+    // exact (h = 0 is the state after leading zero blocks), so the tag is the
+    // reference's (poly1305.rs:213-228).  Blocks are read as one unaligned
+    // 16-byte LDS load each, one block ahead of the multiply.
+    {
+        const uint8_t* blk = lds + (S - 16u * g.z + 16u * v0);
+        const uint32_t tp = g.z / g.k, nv = g.z - tp * g.k;
+        // m holds block j; run(e) steps blocks j .. e-1 (e <= k - 1), each
+        // load issued one block ahead; unrolled by two so that the
+        // prefetched block needs no register copy
+        u32x4 m = ldu16(blk);
+        uint32_t j = 0;
+        auto run = [&](const uint32_t e) {
+            for (; j + 2u <= e; j += 2u) {
+                const u32x4 ma = ldu16(blk + 16u * (j + 1u));
+                __builtin_amdgcn_sched_barrier(0);
+                horner_step(h, m.x, m.y, m.z, m.w, 1u, r0, r1, r2, r3, s1, s2, s3);
+                m = ldu16(blk + 16u * (j + 2u));
+                __builtin_amdgcn_sched_barrier(0);
+                horner_step(h, ma.x, ma.y, ma.z, ma.w, 1u, r0, r1, r2, r3, s1, s2, s3);
+            }
+            if (j < e) {
+                const u32x4 mn = ldu16(blk + 16u * (j + 1u));
+                __builtin_amdgcn_sched_barrier(0);
+                horner_step(h, m.x, m.y, m.z, m.w, 1u, r0, r1, r2, r3, s1, s2, s3);
+                m = mn;
+                ++j;
+            }
+        };
+        run(nv);
+        if (t == tp) h = H32{0u, 0u, 0u, 0u, 0u};
+        run(g.k - 1u);
+        // final block: a partial one carries its pad bit at 8 * rem
+        // (poly1305.rs:216-225; the bytes after the stream are zero)
+        uint32_t pad = 1u;
+        if (rem < 16u && t == PL - 1u) {
+            const uint32_t fb = 1u << (8u * (rem & 3u));
+            const uint32_t fw = rem >> 2;
+            m.x |= fw == 0u ? fb : 0u;
+            m.y |= fw == 1u ? fb : 0u;
+            m.z |= fw == 2u ? fb : 0u;
+            m.w |= fw == 3u ? fb : 0u;
+            pad = 0u;
+        }
+        horner_step(h, m.x, m.y, m.z, m.w, pad, r0, r1, r2, r3, s1, s2, s3);
+        if (t < tp) h = H32{0u, 0u, 0u, 0u, 0u};
+    }
+#else
+    const uint32_t sh = (S & 3u) * 8u;
+    uint32_t pos = S - 16u * g.z + 16u * v0;
+    const uint32_t* l32 = reinterpret_cast<const uint32_t*>(lds);
     for (uint32_t j = 0; j < g.k; ++j) {
         const uint32_t q = pos >> 2;
         const uint32_t a0 = l32[q], a1 = l32[q + 1], a2 = l32[q + 2], a3 = l32[q + 3], a4 = l32[q + 4];
@@ -603,6 +662,7 @@ __device__ __forceinline__ void aead_record(const KParams& p, const uint32_t rec
         horner_step(h, m0, m1, m2, m3, pad, r0, r1, r2, r3, s1, s2, s3);
         pos += 16u;
     }
+#endif
     // radix 2^32 -> 2^26 (h < 2^131)
     F26 f = words_to_f26(h.h0, h.h1, h.h2, h.h3, 0u);
     f.v4 += h.h4 << 24;
@@ -934,7 +994,7 @@ hipError_t launch_compare(const uint8_t* a, uint64_t sa, const uint8_t* b, uint6
 const char* kernel_config() {
 #define SG_STR2(x) #x
 #define SG_STR(x) SG_STR2(x)
-    return "gfx950 sg_aead_kernel v7" "/salu_pre=" SG_STR(SG_SALU_PRE)
+    return "gfx950 sg_aead_kernel v8" "/salu_pre=" SG_STR(SG_SALU_PRE) "/mac_v2=" SG_STR(SG_MAC_V2)
            ": 8 size classes (2..256 lanes per record, one 64-B block per lane, device bucketing, exact class grids), "
            "lane=64B ChaCha block (counter-free round-1 QRs on SALU for wave-uniform records), Poly1305 contiguous-chunk Horner radix-2^32 (clamped r) on min(L,64) lanes + "
            "per-lane r^(k(PL-1-t)) scale + shuffle sum, keying pre-pass";
