@@ -555,11 +555,11 @@ __device__ __forceinline__ void aead_record(const KParams& p, const uint32_t rec
     if (!work || t >= PL) return;
 
     // ---- phase 2: Poly1305 on PL lanes -----------------------------------------
-    // open: lane 0 fetches the received tag now so that its memory latency
+    // open: the finishing lane fetches the received tag now so that its memory latency
     // hides behind the Horner loop instead of stalling the final compare
     uint32_t rx[4] = {0u, 0u, 0u, 0u};
     if constexpr (OPEN) {
-        if (t == 0) {
+        if (t == (SG_MAC_V2 ? PL - 1u : 0u)) {  // the lane that finishes the tag
             const uint8_t* ep = in + n;
             if ((((uintptr_t)ep) & 3u) == 0u) {
                 const uint32_t* e32 = reinterpret_cast<const uint32_t*>(ep);
@@ -677,8 +677,52 @@ __device__ __forceinline__ void aead_record(const KParams& p, const uint32_t rec
         const F26 plo = load_f26(kr + kPowLoOff + 5u * (e & 7u));
         const F26 phi = load_f26(kr + kPowHiOff + 5u * (e >> 3));
         const F26 P = mul_add(phi, plo.v0, plo.v1, plo.v2, plo.v3, plo.v4, f26_zero());
+#if SG_MAC_V2
+        f = mul_add(f, P.v0, P.v1, P.v2, P.v3, P.v4, f26_zero());
+#else
         f = carry_full(mul_add(f, P.v0, P.v1, P.v2, P.v3, P.v4, f26_zero()));
+#endif
     }
+#if SG_MAC_V2
+    // Sum the PL lane terms into the group's last lane with DPP row shifts
+    // (groups of PL <= 16 lanes lie inside one 16-lane row) and the row
+    // broadcasts for 32 and 64.  mul_add leaves limbs < 2^27, so 32 terms sum
+    // below 2^32; one carry pass precedes the last doubling.
+    {
+        auto level = [&](auto dpp) {
+            f.v0 += dpp(f.v0); f.v1 += dpp(f.v1); f.v2 += dpp(f.v2); f.v3 += dpp(f.v3); f.v4 += dpp(f.v4);
+        };
+        auto carry = [&]() {
+            uint32_t c;
+            c = f.v0 >> 26; f.v0 &= M26; f.v1 += c;
+            c = f.v1 >> 26; f.v1 &= M26; f.v2 += c;
+            c = f.v2 >> 26; f.v2 &= M26; f.v3 += c;
+            c = f.v3 >> 26; f.v3 &= M26; f.v4 += c;
+            c = f.v4 >> 26; f.v4 &= M26; f.v0 += c * 5u;
+        };
+        // row_shr:n = 0x110 + n, row_bcast:15 = 0x142, row_bcast:31 = 0x143; only the
+        // group's last lane (31 or 63 for the broadcasts) is read afterwards
+        if constexpr (PL == 2u) carry();
+        level([](uint32_t x) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, true); });
+        if constexpr (PL == 4u) carry();
+        if constexpr (PL >= 4u)
+            level([](uint32_t x) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, true); });
+        if constexpr (PL == 8u) carry();
+        if constexpr (PL >= 8u)
+            level([](uint32_t x) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, true); });
+        if constexpr (PL == 16u) carry();
+        if constexpr (PL >= 16u)
+            level([](uint32_t x) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, true); });
+        if constexpr (PL == 32u) carry();
+        if constexpr (PL >= 32u)
+            level([](uint32_t x) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xf, 0xf, true); });
+        if constexpr (PL == 64u) {
+            carry();
+            level([](uint32_t x) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xf, 0xf, true); });
+        }
+    }
+    if (t != PL - 1u) return;
+#else
     // limbs < 2^26: PL/2 <= 32 of them sum below 2^31, so carry once before the last level
 #pragma unroll
     for (uint32_t d = 1; d < PL; d <<= 1) {
@@ -697,6 +741,7 @@ __device__ __forceinline__ void aead_record(const KParams& p, const uint32_t rec
         f.v4 += __shfl_xor(f.v4, (int)d, 64);
     }
     if (t != 0) return;
+#endif
     uint32_t s[4] = {kr[kSOff + 0], kr[kSOff + 1], kr[kSOff + 2], kr[kSOff + 3]};
     uint32_t tw[4];
     tag_words(f, s, tw);
