@@ -535,10 +535,12 @@ __device__ __forceinline__ void aead_record(const KParams& p, const uint32_t rec
 
         // ---- MAC stream framing: ad || le64(|ad|) || ct || le64(|ct|) --------
         if (t < PL) {
+#if !SG_MAC_V2  // v2 discards the virtual blocks, so [0, S) may hold anything
             const u32x4 zero = {0u, 0u, 0u, 0u};
             st16(lds + 16u * t, zero);  // [0, Z): virtual blocks read zeros
             st16(lds + 16u * (t + PL), zero);
             for (uint32_t i = Z + t; i < S; i += PL) lds[i] = 0;  // gap before the stream start
+#endif
             for (uint32_t i = t; i < adlen + 8u; i += PL) {
                 uint8_t v;
                 if (i < adlen)
