@@ -350,3 +350,66 @@ def test_mixed_batch_graph_capture(gpu, oracle):
         s, n, o, q = int(lay.seq[i]), int(lay.lens[i]), int(lay.in_off[i]), int(lay.out_off[i])
         exp = oracle.seal(k, struct.pack(">Q", s), pt_h[o:o + n], oracle.tls_ad(s, n))
         assert ct_h[q:q + n + 16] == exp, (i, n)
+
+
+@pytest.mark.parametrize("adlen", [13, 0, 3, 29])
+def test_length_sweep_every_mac_geometry(gpu, oracle, adlen):
+    """Every payload length 0..2200 and every 37th length up to 2^14 + 2048 in
+    one mixed batch (all eight size classes, device bucketing), against the
+    oracle byte for byte, then opened.  For TLS AD the sweep takes 252
+    distinct (MAC lanes, leading virtual blocks) pairs, every odd blocks-per-lane
+    k = 1..19, the partially virtual lane at many offsets and final MAC blocks
+    of every length 1..16 (poly1305.rs:213-228).
+    adlen 13 is TLS mode (nonce and AD built on device, tls.rs:103-112); the
+    others pass explicit per-record nonces and AD."""
+    torch = torch_mod()
+    from suruga_amd import batch as B
+
+    lens = np.concatenate([np.arange(0, 2201), np.arange(2201, 16384 + 2049, 37)]).astype(np.uint32)
+    count = len(lens)
+    rng = np.random.default_rng(1000 + adlen)
+    # records 16-byte aligned (vector path) except every 5th, packed at an odd offset
+    in_off = np.zeros(count, dtype=np.uint64)
+    out_off = np.zeros(count, dtype=np.uint64)
+    pi = po = 0
+    for i in range(count):
+        pi += 3 if i % 5 == 4 else (-pi) % 16
+        po += 3 if i % 5 == 4 else (-po) % 16
+        in_off[i], out_off[i] = pi, po
+        pi += int(lens[i])
+        po += int(lens[i]) + 16
+    pt_h = rng.bytes(pi + 16)
+    nonces_h = rng.bytes(8 * count)
+    ads_h = rng.bytes(max(adlen, 1) * count)
+    seqs = np.arange(count, dtype=np.uint64) * 7919
+    dev = lambda a: torch.from_numpy(a.view(np.int64) if a.dtype == np.uint64 else a.view(np.int32)).to("cuda")
+    keys = dev_bytes(KEY).view(1, 32)
+    if adlen == 13:
+        mode = dict(seq=dev(seqs))
+    else:
+        mode = dict(tls=False, nonces=dev_bytes(nonces_h), ads=dev_bytes(ads_h), ad_len=adlen,
+                    ad_stride=max(adlen, 1))
+    ct = torch.zeros(po + 16, dtype=torch.uint8, device="cuda")
+    common = dict(count=count, keys=keys, max_len=int(lens.max()) + 16, **mode)
+    B.seal(B.Batch(inp=dev_bytes(pt_h), out=ct, lens=dev(lens), in_off=dev(in_off), out_off=dev(out_off),
+                   **common))
+    torch.cuda.synchronize()
+    ct_h = host(ct)
+    for i in range(count):
+        n = int(lens[i])
+        if adlen == 13:
+            s = int(seqs[i])
+            nonce, ad = struct.pack(">Q", s), oracle.tls_ad(s, n)
+        else:
+            nonce, ad = nonces_h[8 * i:8 * i + 8], ads_h[i * max(adlen, 1):i * max(adlen, 1) + adlen]
+        exp = oracle.seal(KEY, nonce, pt_h[in_off[i]:in_off[i] + n], ad)
+        assert ct_h[out_off[i]:out_off[i] + n + 16] == exp, (adlen, n)
+    back = torch.zeros(pi + 16, dtype=torch.uint8, device="cuda")
+    st = torch.full((count,), 0xFF, dtype=torch.uint8, device="cuda")
+    B.open_(B.Batch(inp=ct, out=back, lens=dev((lens + 16).astype(np.uint32)), in_off=dev(out_off),
+                    out_off=dev(in_off), status=st, **common))
+    torch.cuda.synchronize()
+    assert host(st) == bytes(count)
+    back_h = host(back)
+    for i in range(count):
+        assert back_h[in_off[i]:in_off[i] + lens[i]] == pt_h[in_off[i]:in_off[i] + lens[i]], (adlen, int(lens[i]))
