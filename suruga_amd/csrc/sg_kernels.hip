@@ -54,6 +54,22 @@ __device__ __forceinline__ u32x4 ld16(const void* p) {
 __device__ __forceinline__ void st16(void* p, u32x4 v) {
     *reinterpret_cast<u32x4*>(__builtin_assume_aligned(p, 16)) = v;
 }
+// streamed record bytes: read once, written once.  SG_NT sets non-temporal
+// hints (1 loads, 2 stores); measured on C1 they cost 5-9 % (loads),
+// 7-12 % (stores) and 40 % (both), so the product leaves them off.
+#ifndef SG_NT
+#define SG_NT 0
+#endif
+__device__ __forceinline__ u32x4 ldg16(const void* p) {
+    const u32x4* q = reinterpret_cast<const u32x4*>(__builtin_assume_aligned(p, 16));
+    if constexpr (SG_NT & 1) return __builtin_nontemporal_load(q);
+    else return *q;
+}
+__device__ __forceinline__ void stg16(void* p, u32x4 v) {
+    u32x4* q = reinterpret_cast<u32x4*>(__builtin_assume_aligned(p, 16));
+    if constexpr (SG_NT & 2) __builtin_nontemporal_store(v, q);
+    else *q = v;
+}
 // 16 bytes at any byte address (LDS: one ds_read_b128 on gfx950)
 typedef u32x4 u32x4_u __attribute__((aligned(1)));
 __device__ __forceinline__ u32x4 ldu16(const void* p) { return *reinterpret_cast<const u32x4_u*>(p); }
@@ -487,8 +503,8 @@ __device__ __forceinline__ void aead_record(const KParams& p, const uint32_t rec
         for (uint32_t b = t; b < nblocks; b += L) {
             const uint32_t off = b << 6;
             if (vec_ok && off + 64u <= n) {
-                const u32x4 d0 = ld16(in + off), d1 = ld16(in + off + 16);
-                const u32x4 d2 = ld16(in + off + 32), d3 = ld16(in + off + 48);
+                const u32x4 d0 = ldg16(in + off), d1 = ldg16(in + off + 16);
+                const u32x4 d2 = ldg16(in + off + 32), d3 = ldg16(in + off + 48);
                 uint32_t ks[16];
                 // data uses blocks 1.. (chacha20_poly1305.rs:52)
                 if constexpr (SG_SALU_PRE && L >= 64u) chacha_block_pre(ks, pre, rk.k, b + 1u, rk.n14, rk.n15);
@@ -497,10 +513,10 @@ __device__ __forceinline__ void aead_record(const KParams& p, const uint32_t rec
                 const u32x4 r1 = d1 ^ u32x4{ks[4], ks[5], ks[6], ks[7]};
                 const u32x4 r2 = d2 ^ u32x4{ks[8], ks[9], ks[10], ks[11]};
                 const u32x4 r3 = d3 ^ u32x4{ks[12], ks[13], ks[14], ks[15]};
-                st16(out + off, r0);
-                st16(out + off + 16, r1);
-                st16(out + off + 32, r2);
-                st16(out + off + 48, r3);
+                stg16(out + off, r0);
+                stg16(out + off + 16, r1);
+                stg16(out + off + 32, r2);
+                stg16(out + off + 48, r3);
                 if constexpr (OPEN) {
                     st16(ct_lds + off, d0);
                     st16(ct_lds + off + 16, d1);
