@@ -181,6 +181,80 @@ __global__ __launch_bounds__(WG) void stream_co(const u32x4* __restrict__ in, u3
     }
 }
 
+// Wave-specialised form: 8 lock-step ChaCha waves (two records' worth of
+// 4 KiB chunks, as stream_co with BAR = 1) plus NMAC waves that stand in for
+// the MAC: between every two barriers of the rounds they issue MACW
+// dependent-pair v_mad_u64_u32 (half-rate, like the Horner step), so every
+// wave of the workgroup hits the same 80 barriers per block.
+template <int NMAC, int MACW>
+__global__ __launch_bounds__(512 + 64 * NMAC) void stream_ws(const u32x4* __restrict__ in, u32x4* __restrict__ out,
+                                                            uint32_t seed, int nblk) {
+    __shared__ u32x4 lds[512 * 4];
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    if (w >= 8) {  // MAC stand-in waves
+        uint64_t a0 = seed + lane, a1 = lane * 3u, a2 = lane ^ 5u, a3 = lane + 7u;
+        uint32_t m = lane | 1u;
+        for (int blk = 0; blk < nblk; ++blk) {
+            for (int g = 0; g < 80; ++g) {
+#pragma unroll
+                for (int i = 0; i < MACW / 4; ++i) {
+                    a0 = (uint64_t)(uint32_t)a0 * m + (a1 >> 32);
+                    a1 = (uint64_t)(uint32_t)a1 * m + (a2 >> 32);
+                    a2 = (uint64_t)(uint32_t)a2 * m + (a3 >> 32);
+                    a3 = (uint64_t)(uint32_t)a3 * m + (a0 >> 32);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                __builtin_amdgcn_s_barrier();
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        if ((a0 ^ a1 ^ a2 ^ a3) == 0x123456789ull) out[threadIdx.x] = u32x4{1u, 2u, 3u, 4u};
+        return;
+    }
+    const uint32_t nw = gridDim.x * 8u;
+    const uint32_t gw = blockIdx.x * 8u + w;
+    u32x4* slot = lds + w * 256;
+    auto phys = [](uint32_t u) { return u ^ ((u >> 4) & 3u); };
+    u32x4 v[4], vn[4];
+    auto gload = [&](u32x4 (&dst)[4], int blk) {
+        const u32x4* p = in + 256ull * ((uint64_t)blk * nw + gw);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) dst[q] = __builtin_nontemporal_load(p + lane + 64 * q);
+    };
+    gload(vn, 0);
+    for (int blk = 0; blk < nblk; ++blk) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = vn[q];
+        if (blk + 1 < nblk) gload(vn, blk + 1);
+        u32x4* po = out + 256ull * ((uint64_t)blk * nw + gw);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) slot[phys(lane + 64 * q)] = v[q];
+        __builtin_amdgcn_wave_barrier();
+        u32x4 d[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) d[q] = slot[phys(4 * lane + q)];
+        uint32_t x[16];
+        x[0] = 0x61707865u; x[1] = 0x3320646eu; x[2] = 0x79622d32u; x[3] = 0x6b206574u;
+#pragma unroll
+        for (int i = 4; i < 12; ++i) x[i] = seed + i;
+        x[12] = gw * 64u + lane + blk; x[13] = 0; x[14] = seed ^ 9; x[15] = seed ^ 10;
+#pragma unroll 1
+        for (int r = 0; r < 10; ++r) dr<1, 1>(x);
+        uint32_t ks[16];
+        ks[0] = x[0] + 0x61707865u; ks[1] = x[1] + 0x3320646eu; ks[2] = x[2] + 0x79622d32u; ks[3] = x[3] + 0x6b206574u;
+#pragma unroll
+        for (int i = 4; i < 12; ++i) ks[i] = x[i] + seed + i;
+        ks[12] = x[12] + gw * 64u + lane + blk; ks[13] = x[13]; ks[14] = x[14] + (seed ^ 9); ks[15] = x[15] + (seed ^ 10);
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int q = 0; q < 4; ++q) slot[phys(4 * lane + q)] = d[q] ^ u32x4{ks[4 * q], ks[4 * q + 1], ks[4 * q + 2], ks[4 * q + 3]};
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int q = 0; q < 4; ++q) po[lane + 64 * q] = slot[phys(lane + 64 * q)];
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
 template <typename F>
 static void timeit(const char* name, double gib, F launch) {
     launch();
@@ -215,6 +289,19 @@ int main() {
 #define RUN(NB, BAR, WG, PF, name) RUNM(NB, BAR, WG, PF, 0, name)
 #define RUNC(BAR, WG, M, SWZ, name) \
     timeit(name, gib, [&] { hipLaunchKernelGGL((stream_co<BAR, WG, M, SWZ>), dim3(threads / WG), dim3(WG), 0, 0, in, out, 1u, nblk); })
+    {  // wave-specialised: 3 workgroups of 8 ChaCha + NMAC waves per CU
+        const int wgs = 256 * 3, nb = 85;
+        const double g2 = (double)wgs * 512 * nb * 64 / (1 << 30);
+#define RUNW(NMAC, MACW, name) \
+    timeit(name, g2, [&] { hipLaunchKernelGGL((stream_ws<NMAC, MACW>), dim3(wgs), dim3(512 + 64 * NMAC), 0, 0, in, out, 1u, nb); })
+        RUNW(0, 4, "ws 8 chacha + 0 mac");
+        RUNW(2, 4, "ws 8 chacha + 2 mac x4");
+        RUNW(2, 8, "ws 8 chacha + 2 mac x8");
+        RUNW(2, 12, "ws 8 chacha + 2 mac x12");
+        RUNW(2, 16, "ws 8 chacha + 2 mac x16");
+        RUNW(4, 12, "ws 8 chacha + 4 mac x12");
+    }
+    RUNC(1, 512, 0, true, "co grp1 WG=512 swz (ref)");
     RUNC(-1, 256, 3, false, "co copy only WG=256");
     RUNC(-1, 1024, 3, false, "co copy only WG=1024");
     RUNC(-1, 256, 0, false, "co cc WG=256");
