@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=4096, help="records in the CPU-baseline sample")
     ap.add_argument("--cpu-seconds", type=float, default=2.0, help="min wall time of the CPU baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--sg-records", type=int, default=16384,
+                    help="records per rank moved by the separately timed RCCL scatter/gather (N > 1; 0 = off)")
     ap.add_argument("--strong", action="store_true",
                     help="strong scaling: --records in total, split across ranks (default: weak, per rank)")
     ap.add_argument("--traffic", default=None,
@@ -129,6 +131,65 @@ def cpu_baseline(args, n):
         "single_thread_gibs": round(one, 4), "cpu": model or platform.processor(),
         "optimised_cpu": ossl,
     }
+
+
+def measure_scatter_gather(args, dist, backend, rank, world, dev, n, count, seq0, seal_b, lib, keys, ws, stream):
+    """North star: RCCL over xGMI only to scatter inputs / gather outputs.
+    Rank 0 holds S = --sg-records plaintext records for every rank, scatters
+    them, each rank seals its slice, rank 0 gathers the sealed records back.
+    Timed apart from the device-resident rate (best of 3, barrier + sync on
+    both sides, MAX over ranks) and checked: every rank's received slice
+    equals its own fill-rule records and rank 0 re-seals each gathered slice's
+    plaintext and compares."""
+    import ctypes as C
+
+    import torch
+
+    from suruga_amd import batch as B
+    from suruga_amd import shard
+
+    S = min(args.sg_records, count)
+    # gloo rehearsals (several ranks on one card) move host tensors
+    cdev = dev if backend == "nccl" else torch.device("cpu")
+    mine = torch.empty(S * n, dtype=torch.uint8, device=cdev)
+    sealed = torch.empty(S * (n + 16), dtype=torch.uint8, device=dev)
+    src_chunks = gather_chunks = None
+    seq_of = lambda r: r * args.records if not args.strong else shard.record_range(args.records, r, world)[0]  # noqa: E731
+    if rank == 0:
+        src_chunks, gather_chunks = [], []
+        for r in range(world):
+            t = torch.empty(S * n, dtype=torch.uint8, device=dev)
+            B.fill_records(t, n, n, S, SEED, j0=seq_of(r))
+            src_chunks.append(t.to(cdev))
+            gather_chunks.append(torch.empty(S * (n + 16), dtype=torch.uint8, device=cdev))
+    sync = torch.cuda.synchronize
+    dd = dev if backend == "nccl" else None
+    scatter_s = shard.timed_collective(dist, lambda: shard.scatter_records(dist, 0, mine, src_chunks), sync=sync,
+                                       device=dd)
+    mine_d = mine.to(dev)
+    ok = bool(torch.equal(mine_d, torch.as_tensor(seal_b.inp[:S * n])))
+    seal_s = B.Batch(count=S, keys=keys, inp=mine_d, out=sealed, uniform_len=n, in_stride=n, out_stride=n + 16,
+                     seq0=seq0, workspace=ws, stream=stream).to_c()
+    B.N.check(lib.sg_seal_batch(C.byref(seal_s)))
+    torch.cuda.synchronize()
+    sealed_c = sealed.to(cdev)
+    gather_s = shard.timed_collective(dist, lambda: shard.gather_records(dist, 0, sealed_c, gather_chunks),
+                                      sync=sync, device=dd)
+    if rank == 0:
+        check = torch.empty(S * (n + 16), dtype=torch.uint8, device=dev)
+        for r in range(world):
+            cs = B.Batch(count=S, keys=keys, inp=src_chunks[r].to(dev), out=check, uniform_len=n, in_stride=n,
+                         out_stride=n + 16, seq0=seq_of(r), workspace=ws, stream=stream).to_c()
+            B.N.check(lib.sg_seal_batch(C.byref(cs)))
+            torch.cuda.synchronize()
+            ok = ok and bool(torch.equal(check, gather_chunks[r].to(dev)))
+    ok_all = sum_over_ranks(dist, 0.0 if ok else 1.0, dd) == 0.0
+    moved_in, moved_out = (world - 1) * S * n, (world - 1) * S * (n + 16)  # bytes that cross the links
+    return {"records_per_rank": S, "backend": "rccl" if backend == "nccl" else backend,
+            "scatter_ms": round(scatter_s * 1e3, 3), "gather_ms": round(gather_s * 1e3, 3),
+            "scatter_GBps": round(moved_in / scatter_s / 1e9, 2), "gather_GBps": round(moved_out / gather_s / 1e9, 2),
+            "verified": ok_all,
+            "note": "root rank 0 -> every rank and back, outside the device-resident value"}
 
 
 def sum_over_ranks(dist, value, device=None):
@@ -245,6 +306,14 @@ def main():
     tm = B.timing_read()
     B.set_timing(False)
 
+    scatter_gather = None
+    if world > 1 and args.sg_records > 0 and args.workload == "c1":
+        try:  # a side measurement: a failure here is reported, not fatal to the device-resident line
+            scatter_gather = measure_scatter_gather(args, dist, backend, rank, world, dev, n, count, seq0, seal_b,
+                                                    lib, keys, ws, stream)
+        except (RuntimeError, ValueError) as e:
+            scatter_gather = {"error": f"{type(e).__name__}: {e}"[:300]}
+
     # seal + open plaintext bytes of all ranks (weak: every rank the same count)
     total_payload_per_step = payload_per_step * world if not args.strong else int(
         sum_over_ranks(dist, payload_per_step, dev if backend == "nccl" else None))
@@ -303,6 +372,8 @@ def main():
             "correct": roundtrip_ok,
             "cpu_baseline": cpu,
         }
+        if scatter_gather is not None:
+            line["scatter_gather"] = scatter_gather
         print(json.dumps(line), flush=True)
     if dist:
         dist.barrier()

@@ -7,6 +7,13 @@ and its own copy of the key table.  Mixed-size batches (C2) are split by
 bytes (prefix sum of lengths), not by record count.  The only communication is
 the timing protocol of the benchmark: a barrier on both sides of the timed
 region and a MAX over ranks of the elapsed time.
+
+When the records start or end on one GPU (a host feeding one device), the
+north star's "RCCL over xGMI only to scatter inputs / gather outputs" applies:
+`scatter_records` / `gather_records` move equal byte slices between a root and
+every rank (torch.distributed scatter/gather: RCCL send/recv over xGMI on
+MI355X, gloo on CPU).  They sit outside the device-resident rate and are timed
+on their own (`timed_collective`, bench.py "scatter_gather").
 """
 from __future__ import annotations
 
@@ -75,3 +82,28 @@ def timed(dist, fn, steps: int, sync=None, device=None) -> float:
     if dist:
         dist.barrier()
     return max_over_ranks(dist, time.perf_counter() - t0, device)
+
+
+def scatter_records(dist, src: int, out, chunks=None):
+    """Rank `src` sends chunks[r] (one tensor per rank, same shape and dtype
+    as `out`) to rank r; every rank receives its slice into `out`."""
+    if dist is None:
+        out.copy_(chunks[0])
+        return out
+    dist.scatter(out, scatter_list=chunks if dist.get_rank() == src else None, src=src)
+    return out
+
+
+def gather_records(dist, dst: int, inp, chunks=None):
+    """Every rank sends `inp`; rank `dst` receives rank r's into chunks[r]."""
+    if dist is None:
+        chunks[0].copy_(inp)
+        return chunks
+    dist.gather(inp, gather_list=chunks if dist.get_rank() == dst else None, dst=dst)
+    return chunks
+
+
+def timed_collective(dist, fn, reps: int = 3, sync=None, device=None) -> float:
+    """Best of `reps` runs of one collective, each bracketed like `timed`
+    (barrier + device sync on both sides, MAX over ranks)."""
+    return min(timed(dist, fn, 1, sync=sync, device=device) for _ in range(reps))

@@ -60,3 +60,8 @@ def test_bench_two_ranks_one_card(gpu, strong):
         assert j["records_per_s"] * j["ms_per_step"] / 1e3 == pytest.approx(4096, rel=1e-3)
     else:
         assert j["records_per_s"] * j["ms_per_step"] / 1e3 == pytest.approx(8192, rel=1e-3)
+    # root scatter -> per-rank seal -> root gather, timed apart and verified (north star: RCCL over xGMI
+    # only to scatter inputs / gather outputs; gloo through host memory in this one-card rehearsal)
+    sg = j["scatter_gather"]
+    assert sg["verified"] and sg["records_per_rank"] == (2048 if strong else 4096)
+    assert sg["scatter_ms"] > 0 and sg["gather_ms"] > 0

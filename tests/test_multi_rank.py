@@ -91,3 +91,40 @@ def test_byte_balanced_ranges_c2(world):
     total = int(np.sum(lens))
     for lo, hi in rs:
         assert abs(int(np.sum(lens[lo:hi])) - total / world) <= 16384
+
+
+def _sg_worker(rank, world, port):
+    """Root rank 0 scatters every rank's plaintext records, each rank seals its
+    slice (oracle on CPU here, sg_seal_batch in bench.py), rank 0 gathers the
+    sealed records: the bytes that come back equal a single-process seal."""
+    import torch
+
+    from oracle_ffi import oracle as get_oracle
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        o = get_oracle()
+        per = 3
+        rec = lambda i: o.fill_record(0x53555255, i, N)  # noqa: E731
+        as_t = lambda b: torch.tensor(list(b), dtype=torch.uint8)  # noqa: E731
+        chunks = [as_t(b"".join(rec(r * per + j) for j in range(per))) for r in range(world)] if rank == 0 else None
+        mine = torch.empty(per * N, dtype=torch.uint8)
+        shard.timed_collective(dist, lambda: shard.scatter_records(dist, 0, mine, chunks), reps=2)
+        assert bytes(mine.numpy()) == b"".join(rec(rank * per + j) for j in range(per))
+        sealed = b""
+        for j in range(per):
+            i = rank * per + j
+            sealed += o.seal(KEY, i.to_bytes(8, "big"), bytes(mine.numpy())[j * N:(j + 1) * N], o.tls_ad(i, N))
+        back = [torch.empty(per * (N + 16), dtype=torch.uint8) for _ in range(world)] if rank == 0 else None
+        shard.gather_records(dist, 0, as_t(sealed), back)
+        if rank == 0:
+            got = b"".join(bytes(t.numpy()) for t in back)
+            exp = b"".join(o.seal(KEY, i.to_bytes(8, "big"), rec(i), o.tls_ad(i, N)) for i in range(world * per))
+            assert got == exp
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_ranks_scatter_seal_gather_gloo():
+    mp.spawn(_sg_worker, args=(2, _free_port()), nprocs=2, join=True)
