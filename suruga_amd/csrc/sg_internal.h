@@ -63,8 +63,8 @@ __host__ __device__ inline uint32_t size_class(uint32_t n) {
 __host__ __device__ constexpr uint32_t class_lanes(uint32_t c) { return 2u << c; }
 __host__ __device__ constexpr uint32_t class_mac_lanes(uint32_t c) { return class_lanes(c) < 64u ? class_lanes(c) : 64u; }
 __host__ __device__ constexpr uint32_t class_max(uint32_t c) { return c < 7u ? 128u << c : 0xffffffffu; }
-// LDS bytes of one record slot: zero region (16 bytes x max virtual blocks
-// 2*PL) | ad || le64 (16-rounded) | ct (64-rounded) | le64(n) + zeros + funnel slack
+// LDS bytes of one record slot: virtual-block space (16 bytes x max virtual blocks
+// 2*PL) | ad || le64 (16-rounded) | ct (64-rounded) | le64(n) + zeros
 __host__ __device__ inline uint32_t lds_rec_bytes(uint32_t cls, uint32_t adlen, uint32_t max_n) {
     const uint32_t PL = class_mac_lanes(cls);
     return 32u * PL + ((adlen + 8u + 15u) & ~15u) + ((max_n + 63u) & ~63u) + 64u;

@@ -33,9 +33,6 @@
 #ifndef SG_SALU_PRE
 #define SG_SALU_PRE 1  // hoist the counter-free part of ChaCha round 1 to the SALU
 #endif
-#ifndef SG_MAC_V2
-#define SG_MAC_V2 1  // MAC loop: unaligned 16-byte LDS block loads, pad bit folded (see aead_record)
-#endif
 
 namespace sg {
 namespace {
@@ -463,13 +460,13 @@ __device__ __forceinline__ uint32_t uniform(uint32_t x) { return __builtin_amdgc
 // Fused seal / open.  A 256-thread workgroup serves RPW = 256 / L records with
 // L lanes each (size classes: L = 16 for n <= 1 KiB, 64 for n <= 4 KiB, 256
 // otherwise); PL = min(L, 64) of them run the MAC.  Per record, in LDS:
-//   [0, S) zeros | S: ad | le64(adlen) | A: ct (n) | le64(n) | zeros
+//   [0, S) virtual-block space | S: ad | le64(adlen) | A: ct (n) | le64(n) | zeros
 // ---------------------------------------------------------------------------
 template <bool OPEN, uint32_t L>
 __device__ __forceinline__ void aead_record(const KParams& p, const uint32_t rec, const bool active,
                                             uint8_t* lds, const uint32_t t) {
     constexpr uint32_t PL = L < 64u ? L : 64u;
-    constexpr uint32_t Z = 32u * PL;  // zero bytes in front: 16 * max z
+    constexpr uint32_t Z = 32u * PL;  // space for the virtual blocks in front: 16 * max z
     uint32_t n = 0;
     bool work = active;
     const uint32_t len = active ? record_len(p, rec) : 0u;
@@ -551,12 +548,6 @@ __device__ __forceinline__ void aead_record(const KParams& p, const uint32_t rec
 
         // ---- MAC stream framing: ad || le64(|ad|) || ct || le64(|ct|) --------
         if (t < PL) {
-#if !SG_MAC_V2  // v2 discards the virtual blocks, so [0, S) may hold anything
-            const u32x4 zero = {0u, 0u, 0u, 0u};
-            st16(lds + 16u * t, zero);  // [0, Z): virtual blocks read zeros
-            st16(lds + 16u * (t + PL), zero);
-            for (uint32_t i = Z + t; i < S; i += PL) lds[i] = 0;  // gap before the stream start
-#endif
             for (uint32_t i = t; i < adlen + 8u; i += PL) {
                 uint8_t v;
                 if (i < adlen)
@@ -565,7 +556,7 @@ __device__ __forceinline__ void aead_record(const KParams& p, const uint32_t rec
                     v = (uint8_t)((uint64_t)adlen >> (8u * (i - adlen)));
                 lds[S + i] = v;
             }
-            // suffix le64(n), then zeros to the end of the last block (+4 funnel bytes)
+            // suffix le64(n), then zeros to the end of the last block
             for (uint32_t i = t; i < 28u; i += PL) ct_lds[n + i] = i < 8u ? (uint8_t)((uint64_t)n >> (8u * i)) : 0;
         }
     }
@@ -580,7 +571,7 @@ __device__ __forceinline__ void aead_record(const KParams& p, const uint32_t rec
     // hides behind the Horner loop instead of stalling the final compare
     uint32_t rx[4] = {0u, 0u, 0u, 0u};
     if constexpr (OPEN) {
-        if (t == (SG_MAC_V2 ? PL - 1u : 0u)) {  // the lane that finishes the tag
+        if (t == PL - 1u) {  // the lane that finishes the tag
             const uint8_t* ep = in + n;
             if ((((uintptr_t)ep) & 3u) == 0u) {
                 const uint32_t* e32 = reinterpret_cast<const uint32_t*>(ep);
@@ -603,7 +594,6 @@ __device__ __forceinline__ void aead_record(const KParams& p, const uint32_t rec
     const uint32_t v0 = t * g.k;
     const uint32_t rem = g.L - 16u * (g.B - 1u);  // bytes in the final block, 1..16
     H32 h = {0u, 0u, 0u, 0u, 0u};
-#if SG_MAC_V2
     // Every block is stepped with the 2^128 pad bit; the virtual blocks (the
     // first z of the record, all in lanes t <= tp = z / k) are then discarded
     // instead of being masked block by block: lanes t < tp hold only virtual
@@ -655,35 +645,6 @@ __device__ __forceinline__ void aead_record(const KParams& p, const uint32_t rec
         horner_step(h, m.x, m.y, m.z, m.w, pad, r0, r1, r2, r3, s1, s2, s3);
         if (t < tp) h = H32{0u, 0u, 0u, 0u, 0u};
     }
-#else
-    const uint32_t sh = (S & 3u) * 8u;
-    uint32_t pos = S - 16u * g.z + 16u * v0;
-    const uint32_t* l32 = reinterpret_cast<const uint32_t*>(lds);
-    for (uint32_t j = 0; j < g.k; ++j) {
-        const uint32_t q = pos >> 2;
-        const uint32_t a0 = l32[q], a1 = l32[q + 1], a2 = l32[q + 2], a3 = l32[q + 3], a4 = l32[q + 4];
-        uint32_t m0 = __builtin_amdgcn_alignbit(a1, a0, sh);
-        uint32_t m1 = __builtin_amdgcn_alignbit(a2, a1, sh);
-        uint32_t m2 = __builtin_amdgcn_alignbit(a3, a2, sh);
-        uint32_t m3 = __builtin_amdgcn_alignbit(a4, a3, sh);
-        uint32_t pad = (v0 + j >= g.z) ? 1u : 0u;  // 2^128 for a full real block
-        if (j + 1u == g.k && rem < 16u) {
-            // the last lane holds the final, partial block: pad bit at 8 * rem
-            // (poly1305.rs:216-225; the bytes after the stream are zero)
-            if (t == PL - 1u) {
-                const uint32_t fb = 1u << (8u * (rem & 3u));
-                const uint32_t fw = rem >> 2;
-                m0 |= fw == 0u ? fb : 0u;
-                m1 |= fw == 1u ? fb : 0u;
-                m2 |= fw == 2u ? fb : 0u;
-                m3 |= fw == 3u ? fb : 0u;
-                pad = 0u;
-            }
-        }
-        horner_step(h, m0, m1, m2, m3, pad, r0, r1, r2, r3, s1, s2, s3);
-        pos += 16u;
-    }
-#endif
     // radix 2^32 -> 2^26 (h < 2^131)
     F26 f = words_to_f26(h.h0, h.h1, h.h2, h.h3, 0u);
     f.v4 += h.h4 << 24;
@@ -698,13 +659,8 @@ __device__ __forceinline__ void aead_record(const KParams& p, const uint32_t rec
         const F26 plo = load_f26(kr + kPowLoOff + 5u * (e & 7u));
         const F26 phi = load_f26(kr + kPowHiOff + 5u * (e >> 3));
         const F26 P = mul_add(phi, plo.v0, plo.v1, plo.v2, plo.v3, plo.v4, f26_zero());
-#if SG_MAC_V2
         f = mul_add(f, P.v0, P.v1, P.v2, P.v3, P.v4, f26_zero());
-#else
-        f = carry_full(mul_add(f, P.v0, P.v1, P.v2, P.v3, P.v4, f26_zero()));
-#endif
     }
-#if SG_MAC_V2
     // Sum the PL lane terms into the group's last lane with DPP row shifts
     // (groups of PL <= 16 lanes lie inside one 16-lane row) and the row
     // broadcasts for 32 and 64.  mul_add leaves limbs < 2^27, so 32 terms sum
@@ -743,26 +699,6 @@ __device__ __forceinline__ void aead_record(const KParams& p, const uint32_t rec
         }
     }
     if (t != PL - 1u) return;
-#else
-    // limbs < 2^26: PL/2 <= 32 of them sum below 2^31, so carry once before the last level
-#pragma unroll
-    for (uint32_t d = 1; d < PL; d <<= 1) {
-        if (2u * d == PL) {
-            uint32_t c;
-            c = f.v0 >> 26; f.v0 &= M26; f.v1 += c;
-            c = f.v1 >> 26; f.v1 &= M26; f.v2 += c;
-            c = f.v2 >> 26; f.v2 &= M26; f.v3 += c;
-            c = f.v3 >> 26; f.v3 &= M26; f.v4 += c;
-            c = f.v4 >> 26; f.v4 &= M26; f.v0 += c * 5u;
-        }
-        f.v0 += __shfl_xor(f.v0, (int)d, 64);
-        f.v1 += __shfl_xor(f.v1, (int)d, 64);
-        f.v2 += __shfl_xor(f.v2, (int)d, 64);
-        f.v3 += __shfl_xor(f.v3, (int)d, 64);
-        f.v4 += __shfl_xor(f.v4, (int)d, 64);
-    }
-    if (t != 0) return;
-#endif
     uint32_t s[4] = {kr[kSOff + 0], kr[kSOff + 1], kr[kSOff + 2], kr[kSOff + 3]};
     uint32_t tw[4];
     tag_words(f, s, tw);
@@ -1060,7 +996,7 @@ hipError_t launch_compare(const uint8_t* a, uint64_t sa, const uint8_t* b, uint6
 const char* kernel_config() {
 #define SG_STR2(x) #x
 #define SG_STR(x) SG_STR2(x)
-    return "gfx950 sg_aead_kernel v8" "/salu_pre=" SG_STR(SG_SALU_PRE) "/mac_v2=" SG_STR(SG_MAC_V2)
+    return "gfx950 sg_aead_kernel v8" "/salu_pre=" SG_STR(SG_SALU_PRE) "/mac_v2=1"
            ": 8 size classes (2..256 lanes per record, one 64-B block per lane, device bucketing, exact class grids), "
            "lane=64B ChaCha block (counter-free round-1 QRs on SALU for wave-uniform records), Poly1305 contiguous-chunk Horner radix-2^32 (clamped r) on min(L,64) lanes + "
            "per-lane r^(k(PL-1-t)) scale + shuffle sum, keying pre-pass";
