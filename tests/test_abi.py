@@ -109,6 +109,17 @@ def test_no_cpu_fallback_in_product():
         assert "import oracle" not in text and "oracle_ffi" not in text, py
 
 
+def test_missing_library_fails_loudly(tmp_path):
+    """A missing HIP library is an ImportError naming the build step, never a
+    silent CPU path (the loader is the product's only way to the kernels)."""
+    code = ("import sys; from pathlib import Path; from suruga_amd import _native as N\n"
+            "try:\n    N.load(Path(sys.argv[1]))\nexcept ImportError as e:\n"
+            "    print('IMPORTERROR', e); raise SystemExit(0)\nraise SystemExit(1)\n")
+    p = subprocess.run([__import__("sys").executable, "-c", code, str(tmp_path / "absent.so")], cwd=ROOT,
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0 and "IMPORTERROR" in p.stdout and "no CPU fallback" in p.stdout, p.stdout + p.stderr
+
+
 def test_record_header_parser_without_gpu(lib):
     """sg_read_records checks headers (tls.rs:218-238) before any device work:
     with no complete valid record in the buffer it returns the header error
