@@ -698,10 +698,22 @@ __device__ __forceinline__ void aead_record(const KParams& p, const uint32_t rec
             level([](uint32_t x) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xf, 0xf, true); });
         }
     }
-    if (t != PL - 1u) return;
-    uint32_t s[4] = {kr[kSOff + 0], kr[kSOff + 1], kr[kSOff + 2], kr[kSOff + 3]};
     uint32_t tw[4];
-    tag_words(f, s, tw);
+    if constexpr (PL == 64u) {
+        // one record per wave: lift the sum out of lane 63 into SGPRs so the
+        // final reduction and s addition run on the scalar unit instead of
+        // occupying the whole wave's VALU for one lane's arithmetic
+        auto lane63 = [](uint32_t x) { return (uint32_t)__builtin_amdgcn_readlane((int)x, 63); };
+        const F26 fs = {lane63(f.v0), lane63(f.v1), lane63(f.v2), lane63(f.v3), lane63(f.v4)};
+        uint32_t s[4] = {uniform(kr[kSOff + 0]), uniform(kr[kSOff + 1]), uniform(kr[kSOff + 2]),
+                         uniform(kr[kSOff + 3])};
+        tag_words(fs, s, tw);
+        if (t != PL - 1u) return;
+    } else {
+        if (t != PL - 1u) return;
+        uint32_t s[4] = {kr[kSOff + 0], kr[kSOff + 1], kr[kSOff + 2], kr[kSOff + 3]};
+        tag_words(f, s, tw);
+    }
 
     if constexpr (!OPEN) {
         uint8_t* tp = out + n;  // ct || tag (chacha20_poly1305.rs:55)
@@ -996,10 +1008,11 @@ hipError_t launch_compare(const uint8_t* a, uint64_t sa, const uint8_t* b, uint6
 const char* kernel_config() {
 #define SG_STR2(x) #x
 #define SG_STR(x) SG_STR2(x)
-    return "gfx950 sg_aead_kernel v8" "/salu_pre=" SG_STR(SG_SALU_PRE) "/mac_v2=1"
+    return "gfx950 sg_aead_kernel v9" "/salu_pre=" SG_STR(SG_SALU_PRE) "/mac_v2=1"
            ": 8 size classes (2..256 lanes per record, one 64-B block per lane, device bucketing, exact class grids), "
-           "lane=64B ChaCha block (counter-free round-1 QRs on SALU for wave-uniform records), Poly1305 contiguous-chunk Horner radix-2^32 (clamped r) on min(L,64) lanes + "
-           "per-lane r^(k(PL-1-t)) scale + shuffle sum, keying pre-pass";
+           "lane=64B ChaCha block (counter-free round-1 QRs on SALU for wave-uniform records), Poly1305 contiguous-chunk "
+           "Horner radix-2^32 (clamped r, unaligned 16-B LDS block loads, folded pad bit) on min(L,64) lanes + per-lane "
+           "r^(k(PL-1-t)) scale + DPP sum, tag finalised on the SALU for one-record waves, keying pre-pass";
 }
 
 }  // namespace sg
