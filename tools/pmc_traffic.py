@@ -104,13 +104,15 @@ def main(tag: str, records: int = 1 << 20, record_bytes: int = 16384):
             traffic[f"{k}_clock_ghz"] = summ[k]["GRBM_GUI_ACTIVE"] / 8 / summ[k]["dispatch_ns"]
         if k in summ and "SQ_INSTS_VALU" in summ[k]:
             traffic[f"{k}_valu_per_record"] = summ[k]["SQ_INSTS_VALU"] / records
-    try:
-        sys.path.insert(0, str(ROOT))
-        from suruga_amd import _native
-
-        traffic["kernels"] = _native.load().sg_build_info().decode()
-    except Exception:  # the summary is still useful without the build string
-        pass
+    # the build string of the library the profiled bench ran (its JSON line in
+    # the kernel-trace log), so a summary can never be stamped with a newer build
+    log = src / "kt_bench.log"
+    for line in (log.read_text(errors="replace").splitlines() if log.exists() else []):
+        if line.startswith("{") and '"kernels"' in line:
+            try:
+                traffic["kernels"] = json.loads(line)["config"]["kernels"]
+            except (ValueError, KeyError):
+                pass
     (dst / f"traffic_{tag}.json").write_text(json.dumps(traffic, indent=1) + "\n")
     print(json.dumps(traffic, indent=1))
 
