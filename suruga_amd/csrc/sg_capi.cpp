@@ -44,6 +44,10 @@ namespace {
 using sg::fail;
 using sg::hip_fail;
 
+#ifndef SG_SINGLE_ZEROCOPY
+#define SG_SINGLE_ZEROCOPY 1
+#endif
+
 struct DeviceState {
     bool init = false;
     bool ok = false;
@@ -294,35 +298,44 @@ static int single(sg_ctx* c, bool open, const uint8_t* nonce, size_t nonce_len, 
 
     std::lock_guard<std::mutex> lk(c->mu);
     SG_HIP(hipSetDevice(c->device));
-    // one H2D copy of nonce | ad | record through the pinned block
     std::memcpy(c->h_in, nonce, 8);
     if (adlen) std::memcpy(c->h_in + sg::kSingleAdOff, ad, adlen);
     if (in_len) std::memcpy(c->h_in + sg::kSingleInOff, in, in_len);
-    SG_HIP(hipMemcpyAsync(c->d_in, c->h_in, sg::kSingleInOff + in_len, hipMemcpyHostToDevice, c->stream));
+    // SG_SINGLE_ZEROCOPY: the kernels read nonce | ad | record from the pinned
+    // block and write status | output into the pinned out block over PCIe (one
+    // record is a few KiB; two copy launches cost more than the transfer);
+    // otherwise one H2D and one D2H copy through device buffers
+    uint8_t* src = c->h_in;
+    uint8_t* dst = c->h_out;
+    if (!SG_SINGLE_ZEROCOPY) {
+        SG_HIP(hipMemcpyAsync(c->d_in, c->h_in, sg::kSingleInOff + in_len, hipMemcpyHostToDevice, c->stream));
+        src = c->d_in;
+        dst = c->d_out;
+    }
 
     sg_batch b;
     std::memset(&b, 0, sizeof b);
     b.count = 1;
     b.keys = c->d_key;
     b.num_keys = 1;
-    b.nonces = c->d_in;
-    b.ads = c->d_in + sg::kSingleAdOff;
+    b.nonces = src;
+    b.ads = src + sg::kSingleAdOff;
     b.ad_len = (uint32_t)adlen;
     b.ad_stride = (uint32_t)adlen;
-    b.in = c->d_in + sg::kSingleInOff;
+    b.in = src + sg::kSingleInOff;
     b.in_stride = in_len;
-    b.out = c->d_out + sg::kSingleOutOff;
+    b.out = dst + sg::kSingleOutOff;
     b.out_stride = in_len + 16;
     b.uniform_len = (uint32_t)in_len;
-    b.status = c->d_out;
+    b.status = dst;
     b.stream = c->stream;
     b.workspace = c->d_ws;
     b.workspace_size = sg_workspace_size(1);
     int rc = open ? sg_open_batch(&b) : sg_seal_batch(&b);
     if (rc != SG_OK) return rc;
-    // one D2H copy of status | output
     const size_t out_len = open ? n : n + SG_MAC_LEN;
-    SG_HIP(hipMemcpyAsync(c->h_out, c->d_out, sg::kSingleOutOff + out_len, hipMemcpyDeviceToHost, c->stream));
+    if (!SG_SINGLE_ZEROCOPY)
+        SG_HIP(hipMemcpyAsync(c->h_out, c->d_out, sg::kSingleOutOff + out_len, hipMemcpyDeviceToHost, c->stream));
     SG_HIP(hipStreamSynchronize(c->stream));
     const uint8_t st = open ? c->h_out[0] : 0;
     if (open && st != 0) {
