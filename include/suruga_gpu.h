@@ -266,6 +266,14 @@ int sg_set_timing(int enable);
 int sg_timing_read(double* seal_ms, double* open_ms, double* keying_ms,
                    uint32_t* n_seal, uint32_t* n_open, uint32_t* n_keying);
 
+/* Kernel form for uniform batches of 8 KiB < n <= 16 KiB records (C1):
+ * 1 = lock-step kernel (two records per 512-thread workgroup, MAC on all 256
+ * lanes), 0 = the size-class kernel used for every other batch.  Both are
+ * bit-exact; the switch exists for A/B measurement and for tests that cover
+ * both.  Initial value: environment SG_LOCKSTEP ("0"/"1"), else the build
+ * default.  Returns the previous setting; a negative argument only queries. */
+int sg_set_lockstep(int enable);
+
 #ifdef __cplusplus
 }
 #endif

@@ -193,6 +193,7 @@ int run_batch(const sg_batch* b, bool open) {
     const uint32_t maxl = b->len ? b->max_len : b->uniform_len;
     const uint32_t max_n = open ? (maxl >= 16u ? maxl - 16u : 0u) : maxl;
     const bool uniform = !b->len || sg::size_class(max_n) == 0u;
+    p.ls = (!b->len && sg::lockstep_enabled() && sg::ls_eligible(max_n, p.ad_len)) ? 1u : 0u;
     uint32_t* lists = p.ws + (size_t)b->count * sg::kKeyRecWords;
     uint32_t* counts = lists + (uint64_t)sg::kNumClasses * b->count;
 
@@ -373,6 +374,11 @@ int sg_compare_records(const uint8_t* a, uint64_t sa, const uint8_t* b, uint64_t
     SG_HIP(sg::launch_compare(a, sa, b, sb, len, count, mism, (hipStream_t)stream));
     if (!stream) SG_HIP(hipStreamSynchronize(nullptr));
     return SG_OK;
+}
+
+int sg_set_lockstep(int enable) {
+    std::lock_guard<std::mutex> lk(g_mu);  // not while a batch is being launched
+    return sg::set_lockstep(enable);
 }
 
 int sg_set_timing(int enable) {

@@ -8,17 +8,20 @@
 namespace sg {
 
 constexpr uint32_t kThreads = 256;        // one record per 256-thread workgroup
-constexpr uint32_t kKeyRecWords = 96;     // per-record keying output (u32 words, 384 B)
+constexpr uint32_t kKeyRecWords = 104;    // per-record keying output (u32 words, 416 B)
 // keying record layout (u32 words): r[4] clamped Poly1305 r (radix 2^32),
 // s[4] (second half of keystream block 0), then with R = r^k (k = MAC blocks
 // per lane, see mac_geom in sg_kernels.hip), in radix 2^26:
 //   lo[8][5] = R^j       j = 0..7
 //   hi[8][5] = R^(8 i)   i = 0..7
-// so that MAC lane t = 8a + b scales its partial sum by R^(63-t) = hi[7-a] lo[7-b].
+// so that MAC lane t = 8a + b scales its partial sum by R^(63-t) = hi[7-a] lo[7-b];
+// for the lock-step kernel (256 MAC lanes per record, KParams::ls) also
+//   wave[3][5] = R^192, R^128, R^64  (wave w of the record scales by wave[w], w < 3)
 constexpr uint32_t kR32Off = 0;
 constexpr uint32_t kSOff = 4;
 constexpr uint32_t kPowLoOff = 8;
 constexpr uint32_t kPowHiOff = 48;
+constexpr uint32_t kWavePowOff = 88;
 
 // Kernel parameters (passed by value as kernarg).
 struct KParams {
@@ -44,7 +47,7 @@ struct KParams {
     uint32_t tls;            // 1 = SG_BATCH_TLS
     uint32_t tls_hdr;        // content_type | major << 8 | minor << 16
     uint32_t lds_rec_bytes;  // LDS bytes per record slot of the launched size class
-    uint32_t pad;
+    uint32_t ls;             // 1: uniform class-7 batch run by the lock-step kernel (256 MAC lanes)
 };
 
 // Size classes of the AEAD kernel: class c (0..7) holds records of
@@ -69,6 +72,21 @@ __host__ __device__ inline uint32_t lds_rec_bytes(uint32_t cls, uint32_t adlen, 
     const uint32_t PL = class_mac_lanes(cls);
     return 32u * PL + ((adlen + 8u + 15u) & ~15u) + ((max_n + 63u) & ~63u) + 64u;
 }
+
+// Lock-step kernel (sg_aead_ls_kernel): two records of one length n per
+// 512-thread workgroup, one 64-byte ChaCha20 block per lane (n <= 16384) and
+// the MAC on all 256 lanes of a record, k = ceil(B / 256) | 1 <= 5 blocks per
+// lane.  LDS slot: [0, 1284) lane accumulators + counter | [.., kLsHead) virtual-block pad |
+// ad || le64(|ad|) (16-rounded) | ct (64-rounded) | le64(n) + zeros.
+constexpr uint32_t kLsHead = 1408;
+__host__ __device__ inline bool ls_eligible(uint32_t n, uint32_t adlen) {
+    return n > 8192u && n <= 16384u && (adlen + 16u + n + 15u) / 16u <= 256u * 5u;
+}
+__host__ __device__ inline uint32_t lds_ls_rec_bytes(uint32_t adlen, uint32_t n) {
+    return kLsHead + ((adlen + 8u + 15u) & ~15u) + ((n + 63u) & ~63u) + 64u;
+}
+bool lockstep_enabled();  // sg_set_lockstep / SG_LOCKSTEP environment switch
+int set_lockstep(int enable);
 
 hipError_t launch_keying(const KParams& p, bool open, hipStream_t s);
 // Seal/open launch.  uniform: every record is in size_class(max_n) (direct

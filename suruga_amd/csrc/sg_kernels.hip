@@ -27,11 +27,22 @@
 // All Poly1305 arithmetic is exact mod p = 2^130 - 5, so the tag equals the
 // reference's sequential Horner result bit for bit.
 #include "sg_internal.h"
+#include "sg_chacha_grp.inc"  // grouped ChaCha20 double round (tools/gen_chacha_grp.py --product)
 
 #include <stdint.h>
+#include <stdlib.h>
 
 #ifndef SG_SALU_PRE
 #define SG_SALU_PRE 1  // hoist the counter-free part of ChaCha round 1 to the SALU
+#endif
+#ifndef SG_LS_NOMAC
+#define SG_LS_NOMAC 0  // timing experiments only: the lock-step kernel skips the MAC (tags are wrong)
+#endif
+#ifndef SG_LS_NOROUNDS
+#define SG_LS_NOROUNDS 0
+#endif
+#ifndef SG_LS_COMPILED
+#define SG_LS_COMPILED 0  // experiments: the lock-step kernel with compiled (unsynchronised) rounds
 #endif
 
 namespace sg {
@@ -413,7 +424,7 @@ __global__ __launch_bounds__(64) void sg_keying_kernel(const KParams p) {
         // R = r^k by square-and-multiply; then R^0..R^7 and R^0, R^8, .., R^56.
         // mul_add outputs are valid multipliers as they stand (limb 1 may exceed
         // 2^26 by < 2^8), so no extra carry passes are needed here.
-        const MacGeom g = mac_geom(p.tls ? 13u : p.ad_len, n, mac_lanes(n));
+        const MacGeom g = mac_geom(p.tls ? 13u : p.ad_len, n, p.ls ? 256u : mac_lanes(n));
         const F26 r = words_to_f26(r0, r1, r2, r3, 0u);
         F26 R = r;
         for (int bit = 30 - __builtin_clz(g.k); bit >= 0; --bit) {
@@ -430,6 +441,14 @@ __global__ __launch_bounds__(64) void sg_keying_kernel(const KParams p) {
         for (int i = 0; i < 8; ++i) {  // hi[i] = R^(8 i)
             store_f26(out + kPowHiOff + 5 * i, x);
             if (i < 7) x = mul_add(x, R8.v0, R8.v1, R8.v2, R8.v3, R8.v4, f26_zero());
+        }
+        if (p.ls) {  // wave factors of the lock-step kernel: R^192, R^128, R^64
+            const F26 R64 = mul_add(x, R8.v0, R8.v1, R8.v2, R8.v3, R8.v4, f26_zero());
+            const F26 R128 = mul_add(R64, R64.v0, R64.v1, R64.v2, R64.v3, R64.v4, f26_zero());
+            const F26 R192 = mul_add(R128, R64.v0, R64.v1, R64.v2, R64.v3, R64.v4, f26_zero());
+            store_f26(out + kWavePowOff + 0, R192);
+            store_f26(out + kWavePowOff + 5, R128);
+            store_f26(out + kWavePowOff + 10, R64);
         }
     }
     __syncthreads();
@@ -778,6 +797,317 @@ __global__ __launch_bounds__(256) void sg_aead_list_kernel(const KParams p, cons
     }
 }
 
+// ---------------------------------------------------------------------------
+// Lock-step form of a uniform 16 KiB-class batch (KParams::ls; every record
+// has the same length n, 8192 < n <= 16384).  Two records per 512-thread
+// workgroup, so each SIMD holds two waves of one workgroup:
+// * the record enters LDS with lane-contiguous 16-byte loads (1 KiB per
+//   wave instruction; a lane that loads its own 64-byte block directly -- the
+//   sg_aead_kernel pattern -- caps read+write at ~3.6 TB/s on MI355X, lane-
+//   contiguous access streams ~5 TB/s, profiles/r01_valu_issue_probes.md);
+// * lane t computes keystream block t + 1 (chacha20_poly1305.rs:52) with the
+//   grouped rounds of sg_chacha_grp.inc -- four adds, four xors, four rotates,
+//   s_barrier -- which keep the two waves of a SIMD in lock-step so that
+//   their full-rate add/xor pair (2 cycles instead of 4);
+// * Poly1305 runs on all 256 lanes (k <= 5 blocks each instead of 17 on one
+//   wave), so no wave carries a long MAC tail that holds the record's LDS:
+//   lane t = 64 w + l scales its Horner sum by R^(64 (3 - w)) (R = r^k) and
+//   adds it into a per-lane LDS accumulator; the last wave scales acc[l] by
+//   R^(63 - l) and sums the lanes with DPP.
+// Measured (profiles/r01_lockstep_ab.md): the rounds run 2.2 ms faster than
+// compiled ones, but the 256-lane MAC costs more than v9's one-wave MAC, so
+// the kernel is 3-5 % slower than sg_aead_kernel on C1: off by default
+// (sg_set_lockstep).
+// Seal: load -> rounds -> ct into LDS -> store + MAC.  Open: load -> MAC over
+// the received ciphertext -> rounds -> plaintext -> store (the reference
+// decrypts unconditionally, chacha20_poly1305.rs:80-82).  Every wave runs the
+// same rounds and barriers whatever its record holds: an inactive slot runs
+// on dummy state.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ F26 wave_sum_to_lane63(F26 f) {
+    auto level = [&](auto dpp) {
+        f.v0 += dpp(f.v0); f.v1 += dpp(f.v1); f.v2 += dpp(f.v2); f.v3 += dpp(f.v3); f.v4 += dpp(f.v4);
+    };
+    auto carry = [&]() {
+        uint32_t c;
+        c = f.v0 >> 26; f.v0 &= M26; f.v1 += c;
+        c = f.v1 >> 26; f.v1 &= M26; f.v2 += c;
+        c = f.v2 >> 26; f.v2 &= M26; f.v3 += c;
+        c = f.v3 >> 26; f.v3 &= M26; f.v4 += c;
+        c = f.v4 >> 26; f.v4 &= M26; f.v0 += c * 5u;
+    };
+    // row_shr:1,2,4,8 then row_bcast:15 and row_bcast:31 (see aead_record)
+    level([](uint32_t x) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, true); });
+    level([](uint32_t x) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, true); });
+    level([](uint32_t x) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, true); });
+    level([](uint32_t x) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, true); });
+    level([](uint32_t x) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xf, 0xf, true); });
+    carry();
+    level([](uint32_t x) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xf, 0xf, true); });
+    return f;
+}
+
+// Poly1305 on all 256 lanes of a record: lane t = 64 w + l runs the Horner
+// chain of its k blocks and adds h_t R^(64 (3 - w)) into acc[l]; ls_finish
+// then forms sum_l acc[l] R^(63 - l) = sum_t h_t R^(255 - t).  Exactly the virtual-block scheme of aead_record with
+// PL = 256 (the keying kernel derives k with the same PL when p.ls is set).
+__device__ __forceinline__ void ls_mac(const KParams& p, const uint32_t rec, const uint32_t n, const uint32_t adlen,
+                                       const uint8_t* slot, const uint32_t S, const uint32_t t, const uint32_t w,
+                                       uint32_t* acc) {
+    const uint32_t lane = t & 63u;
+    const MacGeom g = mac_geom(adlen, n, 256u);
+    const uint32_t* kr = p.ws + (uint64_t)rec * kKeyRecWords;
+    const uint32_t r0 = uniform(kr[kR32Off + 0]), r1 = uniform(kr[kR32Off + 1]);
+    const uint32_t r2 = uniform(kr[kR32Off + 2]), r3 = uniform(kr[kR32Off + 3]);
+    const uint32_t s1 = r1 + (r1 >> 2), s2 = r2 + (r2 >> 2), s3 = r3 + (r3 >> 2);
+    const uint32_t v0 = t * g.k;
+    const uint32_t tp = g.z / g.k, nv = g.z - tp * g.k;
+    const uint32_t rem = g.L - 16u * (g.B - 1u);
+    // lanes t < tp hold only virtual blocks (read anything, discarded); lane
+    // tp reads nv virtual blocks in front of the stream (kLsHead leaves room)
+    const uint8_t* blk = t < tp ? slot + S : (t == tp ? slot + S - 16u * nv : slot + S + 16u * (v0 - g.z));
+    H32 h = {0u, 0u, 0u, 0u, 0u};
+    u32x4 m = ldu16(blk);
+    uint32_t j = 0;
+    auto run = [&](const uint32_t e) {
+        for (; j + 2u <= e; j += 2u) {
+            const u32x4 ma = ldu16(blk + 16u * (j + 1u));
+            __builtin_amdgcn_sched_barrier(0);
+            horner_step(h, m.x, m.y, m.z, m.w, 1u, r0, r1, r2, r3, s1, s2, s3);
+            m = ldu16(blk + 16u * (j + 2u));
+            __builtin_amdgcn_sched_barrier(0);
+            horner_step(h, ma.x, ma.y, ma.z, ma.w, 1u, r0, r1, r2, r3, s1, s2, s3);
+        }
+        if (j < e) {
+            const u32x4 mn = ldu16(blk + 16u * (j + 1u));
+            __builtin_amdgcn_sched_barrier(0);
+            horner_step(h, m.x, m.y, m.z, m.w, 1u, r0, r1, r2, r3, s1, s2, s3);
+            m = mn;
+            ++j;
+        }
+    };
+    run(nv);
+    if (t == tp) h = H32{0u, 0u, 0u, 0u, 0u};
+    run(g.k - 1u);
+    uint32_t pad = 1u;
+    if (rem < 16u && t == 255u) {  // partial final block: pad bit at 8 * rem (poly1305.rs:216-225)
+        const uint32_t fb = 1u << (8u * (rem & 3u));
+        const uint32_t fw = rem >> 2;
+        m.x |= fw == 0u ? fb : 0u;
+        m.y |= fw == 1u ? fb : 0u;
+        m.z |= fw == 2u ? fb : 0u;
+        m.w |= fw == 3u ? fb : 0u;
+        pad = 0u;
+    }
+    horner_step(h, m.x, m.y, m.z, m.w, pad, r0, r1, r2, r3, s1, s2, s3);
+    if (t < tp) h = H32{0u, 0u, 0u, 0u, 0u};
+    F26 f = words_to_f26(h.h0, h.h1, h.h2, h.h3, 0u);
+    f.v4 += h.h4 << 24;
+    {
+        const uint32_t c = f.v4 >> 26;
+        f.v4 &= M26;
+        f.v0 += c * 5u;
+    }
+    if (w < 3u) {  // wave factor R^(64 (3 - w))
+        const uint32_t* q = kr + kWavePowOff + 5u * w;
+        f = mul_add(f, uniform(q[0]), uniform(q[1]), uniform(q[2]), uniform(q[3]), uniform(q[4]), f26_zero());
+    }
+    // lane l of every wave shares the factor R^(63 - l): add the four waves'
+    // terms first (LDS atomics, limbs < 2^27 each), scale once (ls_finish)
+    uint32_t* a = acc + 5u * lane;
+    __hip_atomic_fetch_add(a + 0, f.v0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_fetch_add(a + 1, f.v1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_fetch_add(a + 2, f.v2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_fetch_add(a + 3, f.v3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_fetch_add(a + 4, f.v4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// sum_l acc[l] R^(63 - l) + s -> tag; seal appends it (chacha20_poly1305.rs:55),
+// open compares all 16 bytes (:84-93) and writes the record status.
+template <bool OPEN>
+__device__ __forceinline__ void ls_finish(const KParams& p, const uint32_t rec, const uint32_t n, const uint8_t* in,
+                                          uint8_t* out, const uint32_t* acc, const uint32_t lane) {
+    const uint32_t* kr = p.ws + (uint64_t)rec * kKeyRecWords;
+    F26 f = load_f26(acc + 5u * lane);
+    {  // limbs < 2^28 here: one carry pass before they enter mul_add
+        uint32_t c;
+        c = f.v0 >> 26; f.v0 &= M26; f.v1 += c;
+        c = f.v1 >> 26; f.v1 &= M26; f.v2 += c;
+        c = f.v2 >> 26; f.v2 &= M26; f.v3 += c;
+        c = f.v3 >> 26; f.v3 &= M26; f.v4 += c;
+        c = f.v4 >> 26; f.v4 &= M26; f.v0 += c * 5u;
+    }
+    {  // lane factor R^(63 - lane) = hi[e >> 3] lo[e & 7]
+        const uint32_t e = 63u - lane;
+        const F26 plo = load_f26(kr + kPowLoOff + 5u * (e & 7u));
+        const F26 phi = load_f26(kr + kPowHiOff + 5u * (e >> 3));
+        const F26 P = mul_add(phi, plo.v0, plo.v1, plo.v2, plo.v3, plo.v4, f26_zero());
+        f = mul_add(f, P.v0, P.v1, P.v2, P.v3, P.v4, f26_zero());
+    }
+    f = wave_sum_to_lane63(f);
+    auto lane63 = [](uint32_t x) { return (uint32_t)__builtin_amdgcn_readlane((int)x, 63); };
+    f = F26{lane63(f.v0), lane63(f.v1), lane63(f.v2), lane63(f.v3), lane63(f.v4)};
+    uint32_t s[4] = {uniform(kr[kSOff + 0]), uniform(kr[kSOff + 1]), uniform(kr[kSOff + 2]), uniform(kr[kSOff + 3])};
+    uint32_t tw[4];
+    tag_words(f, s, tw);
+    if (lane != 0u) return;
+    if constexpr (!OPEN) {
+        uint8_t* tp = out + n;
+        if ((((uintptr_t)tp) & 3u) == 0u) {
+            uint32_t* t32 = reinterpret_cast<uint32_t*>(tp);
+            t32[0] = tw[0]; t32[1] = tw[1]; t32[2] = tw[2]; t32[3] = tw[3];
+        } else {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) tp[i] = (uint8_t)(tw[i >> 2] >> (8 * (i & 3)));
+        }
+    } else {
+        uint32_t rx[4] = {0u, 0u, 0u, 0u};
+        const uint8_t* ep = in + n;
+        if ((((uintptr_t)ep) & 3u) == 0u) {
+            const uint32_t* e32 = reinterpret_cast<const uint32_t*>(ep);
+            rx[0] = e32[0]; rx[1] = e32[1]; rx[2] = e32[2]; rx[3] = e32[3];
+        } else {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) rx[i >> 2] |= (uint32_t)ep[i] << (8 * (i & 3));
+        }
+        const uint32_t diff = (rx[0] ^ tw[0]) | (rx[1] ^ tw[1]) | (rx[2] ^ tw[2]) | (rx[3] ^ tw[3]);
+        p.status[rec] = diff != 0u ? 1u : 0u;
+    }
+}
+
+// le64(n) and zeros to the end of the last MAC block, after the ciphertext
+__device__ __forceinline__ void ls_suffix(uint8_t* ct, const uint32_t n) {
+    if ((n & 3u) == 0u) {
+        uint32_t* q = reinterpret_cast<uint32_t*>(ct + n);
+        q[0] = n; q[1] = 0u; q[2] = 0u; q[3] = 0u; q[4] = 0u; q[5] = 0u; q[6] = 0u;
+    } else {
+        for (uint32_t i = 0; i < 28u; ++i) ct[n + i] = i < 8u ? (uint8_t)((uint64_t)n >> (8u * i)) : 0;
+    }
+}
+
+template <bool OPEN>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8, 8))) void sg_aead_ls_kernel(const KParams p) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const uint32_t g = __builtin_amdgcn_readfirstlane(threadIdx.x >> 8);
+    const uint32_t t = threadIdx.x & 255u;
+    const uint32_t w = __builtin_amdgcn_readfirstlane(t >> 6), lane = t & 63u;
+    const uint32_t rec = blockIdx.x * 2u + g;
+    const bool active = rec < p.count;
+    uint8_t* slot = lds + g * p.lds_rec_bytes;
+    uint32_t* acc = reinterpret_cast<uint32_t*>(slot);  // [64][5] lane accumulators, then the arrival counter
+    const uint32_t n = OPEN ? p.uniform_len - 16u : p.uniform_len;
+    const uint32_t adlen = p.tls ? 13u : p.ad_len;
+    const uint32_t A = kLsHead + ((adlen + 8u + 15u) & ~15u);
+    const uint32_t S = A - adlen - 8u;  // stream start
+    uint8_t* ct = slot + A;
+    const uint8_t* in = p.in;
+    uint8_t* out = p.out;
+    RecKey rk = {};
+    if (active) {
+        in = p.in + (p.in_off ? p.in_off[rec] : p.in_stride * rec);
+        out = p.out + (p.out_off ? p.out_off[rec] : p.out_stride * rec);
+        rk = record_key(p, rec);
+        acc[t] = 0u;
+        if (t < 65u) acc[256u + t] = 0u;  // the rest of acc and the arrival counter acc[320]
+        // ---- the record into LDS, lane-contiguous ----
+        const uint32_t tail = n & ~15u;
+        if ((((uintptr_t)in) & 15u) == 0u) {
+#pragma unroll
+            for (uint32_t q = 0; q < 4u; ++q) {
+                const uint32_t off = 4096u * w + 16u * (lane + 64u * q);
+                if (off + 16u <= n) st16(ct + off, ldg16(in + off));
+            }
+            if (t < (n & 15u)) ct[tail + t] = in[tail + t];
+        } else {
+#pragma unroll 1
+            for (uint32_t i = t; i < n; i += 256u) ct[i] = in[i];
+        }
+        // ---- MAC stream framing: ad || le64(|ad|) || ct || le64(|ct|) ----
+        for (uint32_t i = t; i < adlen + 8u; i += 256u) {
+            uint8_t v;
+            if (i < adlen)
+                v = p.tls ? tls_ad_byte(rk.seq, p.tls_hdr, n, i) : p.ads[(uint64_t)p.ad_stride * rec + i];
+            else
+                v = (uint8_t)((uint64_t)adlen >> (8u * (i - adlen)));
+            slot[S + i] = v;
+        }
+        if constexpr (OPEN) {
+            if (t == 0u) ls_suffix(ct, n);
+        }
+    }
+    __syncthreads();
+    if constexpr (OPEN) {
+        if (active && !SG_LS_NOMAC) ls_mac(p, rec, n, adlen, slot, S, t, w, acc);
+        __syncthreads();  // every MAC read is done before the plaintext replaces the ciphertext
+    }
+    // ---- keystream block t + 1 in lock-step; XOR in LDS ----
+    const uint32_t off = 64u * t;
+    const bool mine = active && off < n;
+    u32x4 d0 = {}, d1 = {}, d2 = {}, d3 = {};
+    if (mine) {
+        d0 = ld16(ct + off); d1 = ld16(ct + off + 16u); d2 = ld16(ct + off + 32u); d3 = ld16(ct + off + 48u);
+    }
+    uint32_t x[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u, rk.k[0], rk.k[1], rk.k[2], rk.k[3],
+                      rk.k[4],     rk.k[5],     rk.k[6],     rk.k[7],     t + 1u,  0u,      rk.n14,  rk.n15};
+#if SG_LS_NOROUNDS  // experiment: no rounds (the memory path alone; output is wrong)
+#elif SG_LS_COMPILED  // experiment: compiled rounds, no lock-step barriers
+    {
+        uint32_t ks[16];
+        chacha_block(ks, rk.k, t + 1u, rk.n14, rk.n15);
+        for (int i = 0; i < 16; ++i) x[i] = ks[i] - (i < 4 ? (i == 0 ? 0x61707865u : i == 1 ? 0x3320646eu : i == 2 ? 0x79622d32u : 0x6b206574u)
+                                                         : i < 12 ? rk.k[i - 4] : i == 12 ? t + 1u : i == 13 ? 0u : i == 14 ? rk.n14 : rk.n15);
+    }
+#else
+#pragma unroll 1
+    for (int r = 0; r < 10; ++r)
+        asm volatile(SG_CHACHA_DR_NB1_BAR1
+                     : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]),
+                       "+v"(x[7]), "+v"(x[8]), "+v"(x[9]), "+v"(x[10]), "+v"(x[11]), "+v"(x[12]), "+v"(x[13]),
+                       "+v"(x[14]), "+v"(x[15]));
+#endif
+    if (mine) {
+        d0 ^= u32x4{x[0] + 0x61707865u, x[1] + 0x3320646eu, x[2] + 0x79622d32u, x[3] + 0x6b206574u};
+        d1 ^= u32x4{x[4] + rk.k[0], x[5] + rk.k[1], x[6] + rk.k[2], x[7] + rk.k[3]};
+        d2 ^= u32x4{x[8] + rk.k[4], x[9] + rk.k[5], x[10] + rk.k[6], x[11] + rk.k[7]};
+        d3 ^= u32x4{x[12] + t + 1u, x[13], x[14] + rk.n14, x[15] + rk.n15};
+        st16(ct + off, d0); st16(ct + off + 16u, d1); st16(ct + off + 32u, d2); st16(ct + off + 48u, d3);
+    }
+    if constexpr (!OPEN) {
+        // the suffix lies behind the last (possibly partial) block: written by that block's lane
+        if (active && t == ((n >> 6) < 255u ? (n >> 6) : 255u)) ls_suffix(ct, n);
+    }
+    __syncthreads();
+    // ---- the output leaves lane-contiguous ----
+    if (active) {
+        const uint32_t tail = n & ~15u;
+        if ((((uintptr_t)out) & 15u) == 0u) {
+#pragma unroll
+            for (uint32_t q = 0; q < 4u; ++q) {
+                const uint32_t o = 4096u * w + 16u * (lane + 64u * q);
+                if (o + 16u <= n) stg16(out + o, ld16(ct + o));
+            }
+            if (t < (n & 15u)) out[tail + t] = ct[tail + t];
+        } else {
+#pragma unroll 1
+            for (uint32_t i = t; i < n; i += 256u) out[i] = ct[i];
+        }
+    }
+    if constexpr (!OPEN) {
+        if (!active || SG_LS_NOMAC) return;
+        ls_mac(p, rec, n, adlen, slot, S, t, w, acc);
+        // the last wave of the record to finish scales and sums the accumulators
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        uint32_t old = 0u;
+        if (lane == 63u) old = __hip_atomic_fetch_add(acc + 320, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+        old = (uint32_t)__builtin_amdgcn_readlane((int)old, 63);
+        if (old != 3u) return;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        ls_finish<false>(p, rec, n, in, out, acc, lane);
+    } else {
+        if (active && w == (rec & 3u) && !SG_LS_NOMAC) ls_finish<true>(p, rec, n, in, out, acc, lane);
+    }
+}
+
 // Size-class bucketing.  A 1024-thread workgroup classifies 4096 records:
 // per-wave ballots, then one device atomic per class per workgroup (a single
 // counter word takes only ~88 atomics/us, so per-wave atomics cost ~0.5 ms
@@ -946,6 +1276,12 @@ hipError_t launch_class(uint32_t c, const KParams& q, const uint32_t* list, cons
 template <bool OPEN>
 hipError_t launch_aead_t(const KParams& p, uint32_t max_n, bool uniform, uint32_t* lists, uint32_t* counts,
                          hipStream_t s) {
+    if (uniform && p.ls) {  // uniform 16 KiB-class batch: lock-step kernel, two records per workgroup
+        KParams q = p;
+        q.lds_rec_bytes = lds_ls_rec_bytes(q.ad_len, max_n);
+        hipLaunchKernelGGL(sg_aead_ls_kernel<OPEN>, dim3((p.count + 1u) / 2u), dim3(512), 2u * q.lds_rec_bytes, s, q);
+        return hipGetLastError();
+    }
     if (uniform) {  // every record in one class: direct launch
         KParams q = p;
         const uint32_t c = size_class(max_n);
@@ -1005,9 +1341,34 @@ hipError_t launch_compare(const uint8_t* a, uint64_t sa, const uint8_t* b, uint6
     return hipGetLastError();
 }
 
+#ifndef SG_LOCKSTEP_DEFAULT
+#define SG_LOCKSTEP_DEFAULT 0
+#endif
+static int g_lockstep = -1;  // -1: not read from the environment yet
+bool lockstep_enabled() {
+    if (__atomic_load_n(&g_lockstep, __ATOMIC_ACQUIRE) < 0) {
+        const char* e = getenv("SG_LOCKSTEP");
+        int expect = -1;
+        __atomic_compare_exchange_n(&g_lockstep, &expect, e ? (e[0] == '1' ? 1 : 0) : (SG_LOCKSTEP_DEFAULT ? 1 : 0),
+                                    false, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE);
+    }
+    return __atomic_load_n(&g_lockstep, __ATOMIC_ACQUIRE) == 1;
+}
+int set_lockstep(int enable) {
+    const int prev = lockstep_enabled() ? 1 : 0;
+    if (enable >= 0) __atomic_store_n(&g_lockstep, enable ? 1 : 0, __ATOMIC_RELEASE);
+    return prev;
+}
+
 const char* kernel_config() {
 #define SG_STR2(x) #x
 #define SG_STR(x) SG_STR2(x)
+    if (lockstep_enabled())
+        return "gfx950 sg_aead_kernel v10" "/salu_pre=" SG_STR(SG_SALU_PRE) "/mac_v2=1/lockstep=1"
+               ": uniform 8-16 KiB batches on sg_aead_ls_kernel (two records per 512-thread workgroup, lane-contiguous "
+               "loads/stores through LDS, grouped lock-step ChaCha20 rounds with s_barrier per rotate group, Poly1305 on "
+               "all 256 lanes: k<=5 blocks per lane, per-wave R^(64(3-w)) scaling into per-lane LDS accumulators, one "
+               "R^(63-lane) scaling + DPP sum); other batches: 8 size classes as v9, keying pre-pass";
     return "gfx950 sg_aead_kernel v9" "/salu_pre=" SG_STR(SG_SALU_PRE) "/mac_v2=1"
            ": 8 size classes (2..256 lanes per record, one 64-B block per lane, device bucketing, exact class grids), "
            "lane=64B ChaCha block (counter-free round-1 QRs on SALU for wave-uniform records), Poly1305 contiguous-chunk "

@@ -413,3 +413,70 @@ def test_length_sweep_every_mac_geometry(gpu, oracle, adlen):
     back_h = host(back)
     for i in range(count):
         assert back_h[in_off[i]:in_off[i] + lens[i]] == pt_h[in_off[i]:in_off[i] + lens[i]], (adlen, int(lens[i]))
+
+
+# ---------------------------------------------------------------------------
+# lock-step kernel (uniform batches of 8 KiB < n <= 16 KiB, sg_aead_ls_kernel)
+# ---------------------------------------------------------------------------
+LS_LENGTHS = [8193, 8200, 9000, 10240, 12287, 12288, 12289, 16320, 16321, 16383, 16384]
+
+
+@pytest.fixture(params=[1, 0], ids=["lockstep", "sizeclass"])
+def kernel_form(request, gpu):
+    from suruga_amd import _native as N
+
+    lib = N.load()
+    prev = lib.sg_set_lockstep(request.param)
+    assert lib.sg_set_lockstep(-1) == request.param
+    yield request.param
+    lib.sg_set_lockstep(prev)
+
+
+@pytest.mark.parametrize("adlen", [13, 0, 7, 255])
+def test_lockstep_uniform_geometries(gpu, oracle, kernel_form, adlen):
+    """Uniform batches over every MAC geometry the lock-step kernel takes
+    (k = 3 or 5 blocks per lane, 0..255 leading virtual blocks, final blocks
+    of many lengths), TLS and explicit AD (0..255 bytes), 16-byte aligned
+    records and records at odd strides (byte-granular load/store paths), an odd
+    record count (an inactive slot in the last workgroup), and a tampered tag;
+    both kernel forms against the oracle byte for byte."""
+    torch = torch_mod()
+    from suruga_amd import batch as B
+
+    keys = dev_bytes(KEY).view(1, 32)
+    for n in LS_LENGTHS:
+        for skew in (0, 3):
+            count = 5
+            rng = np.random.default_rng(n * 7 + skew + adlen)
+            si, so = n + skew, n + 16 + skew
+            pt_h = rng.bytes(si * count)
+            nonces_h = rng.bytes(8 * count)
+            ads_h = rng.bytes(max(adlen, 1) * count)
+            seq0 = 0xFFFFFFFE
+            if adlen == 13:
+                mode = dict(seq0=seq0)
+            else:
+                mode = dict(tls=False, nonces=dev_bytes(nonces_h), ads=dev_bytes(ads_h), ad_len=adlen,
+                            ad_stride=max(adlen, 1))
+            ct = torch.zeros(so * count, dtype=torch.uint8, device="cuda")
+            B.seal(B.Batch(count=count, keys=keys, inp=dev_bytes(pt_h), out=ct, uniform_len=n, in_stride=si,
+                           out_stride=so, **mode))
+            torch.cuda.synchronize()
+            ct_h = bytearray(host(ct))
+            for i in range(count):
+                if adlen == 13:
+                    nonce, ad = struct.pack(">Q", seq0 + i), oracle.tls_ad(seq0 + i, n)
+                else:
+                    nonce, ad = nonces_h[8 * i:8 * i + 8], ads_h[i * max(adlen, 1):i * max(adlen, 1) + adlen]
+                exp = oracle.seal(KEY, nonce, pt_h[i * si:i * si + n], ad)
+                assert bytes(ct_h[i * so:i * so + n + 16]) == exp, (kernel_form, adlen, n, skew, i)
+            ct_h[2 * so + n + 5] ^= 0x40  # record 2: tag byte
+            back = torch.zeros(si * count, dtype=torch.uint8, device="cuda")
+            st = torch.full((count,), 0xFF, dtype=torch.uint8, device="cuda")
+            B.open_(B.Batch(count=count, keys=keys, inp=dev_bytes(bytes(ct_h)), out=back, uniform_len=n + 16,
+                            in_stride=so, out_stride=si, status=st, **mode))
+            torch.cuda.synchronize()
+            assert host(st) == bytes([0, 0, 1, 0, 0]), (kernel_form, adlen, n, skew)
+            back_h = host(back)
+            for i in range(count):  # decrypted unconditionally (chacha20_poly1305.rs:80-82)
+                assert back_h[i * si:i * si + n] == pt_h[i * si:i * si + n], (kernel_form, adlen, n, skew, i)
