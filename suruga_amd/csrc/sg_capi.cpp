@@ -194,7 +194,7 @@ int run_batch(const sg_batch* b, bool open) {
     const uint32_t max_n = open ? (maxl >= 16u ? maxl - 16u : 0u) : maxl;
     const bool uniform = !b->len || sg::size_class(max_n) == 0u;
     p.ls = (!b->len && sg::lockstep_enabled() && sg::ls_eligible(max_n, p.ad_len)) ? 1u : 0u;
-    uint32_t* lists = p.ws + (size_t)b->count * sg::kKeyRecWords;
+    uint32_t* lists = p.ws + (size_t)b->count * sg::kKeyRecWordsMax;
     uint32_t* counts = lists + (uint64_t)sg::kNumClasses * b->count;
 
     hipEvent_t e[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -234,7 +234,7 @@ const char* sg_last_error(void) { return g_err.c_str(); }
 const char* sg_build_info(void) { return sg::kernel_config(); }
 size_t sg_workspace_size(uint32_t count) {
     // keying records, one list per size class, one list counter per class
-    return (size_t)count * (sg::kKeyRecWords + sg::kNumClasses) * 4u + sg::kNumClasses * 4u;
+    return (size_t)count * (sg::kKeyRecWordsMax + sg::kNumClasses) * 4u + sg::kNumClasses * 4u;
 }
 
 sg_ctx* sg_ctx_new(const uint8_t key[32], int device) {

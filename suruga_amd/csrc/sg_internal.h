@@ -15,13 +15,20 @@ constexpr uint32_t kKeyRecWords = 104;    // per-record keying output (u32 words
 //   lo[8][5] = R^j       j = 0..7
 //   hi[8][5] = R^(8 i)   i = 0..7
 // so that MAC lane t = 8a + b scales its partial sum by R^(63-t) = hi[7-a] lo[7-b];
-// for the lock-step kernel (256 MAC lanes per record, KParams::ls) also
-//   wave[3][5] = R^192, R^128, R^64  (wave w of the record scales by wave[w], w < 3)
+// The lock-step kernel (KParams::ls, MFMA Poly1305, k from PL = 64 as above)
+// uses a longer record (kKeyRecWordsLs words) that appends, radix 2^26:
+//   rs[8][5]  = r^j        j = 0..7
+//   rm[6][5]  = r^(8 i)    i = 0..5     (r^e = rm[e >> 3] rs[e & 7], e <= 47)
+//   ctot[5]   = the record's constant term of the MFMA evaluation (mfma_mac)
 constexpr uint32_t kR32Off = 0;
 constexpr uint32_t kSOff = 4;
 constexpr uint32_t kPowLoOff = 8;
 constexpr uint32_t kPowHiOff = 48;
-constexpr uint32_t kWavePowOff = 88;
+constexpr uint32_t kRSmallOff = 88;
+constexpr uint32_t kRMidOff = 128;
+constexpr uint32_t kCtotOff = 158;
+constexpr uint32_t kKeyRecWordsLs = 164;
+constexpr uint32_t kKeyRecWordsMax = kKeyRecWordsLs;
 
 // Kernel parameters (passed by value as kernarg).
 struct KParams {
@@ -39,7 +46,7 @@ struct KParams {
     uint64_t out_stride;
     const uint32_t* len;
     uint8_t* status;
-    uint32_t* ws;            // count * kKeyRecWords (keying records)
+    uint32_t* ws;            // count * kKeyRecWords (kKeyRecWordsLs when ls) keying records
     uint32_t uniform_len;
     uint32_t count;
     uint32_t ad_len;         // explicit mode
@@ -47,7 +54,7 @@ struct KParams {
     uint32_t tls;            // 1 = SG_BATCH_TLS
     uint32_t tls_hdr;        // content_type | major << 8 | minor << 16
     uint32_t lds_rec_bytes;  // LDS bytes per record slot of the launched size class
-    uint32_t ls;             // 1: uniform class-7 batch run by the lock-step kernel (256 MAC lanes)
+    uint32_t ls;             // 1: uniform class-7 batch run by the lock-step kernel (MFMA Poly1305)
 };
 
 // Size classes of the AEAD kernel: class c (0..7) holds records of
@@ -74,13 +81,16 @@ __host__ __device__ inline uint32_t lds_rec_bytes(uint32_t cls, uint32_t adlen, 
 }
 
 // Lock-step kernel (sg_aead_ls_kernel): two records of one length n per
-// 512-thread workgroup, one 64-byte ChaCha20 block per lane (n <= 16384) and
-// the MAC on all 256 lanes of a record, k = ceil(B / 256) | 1 <= 5 blocks per
-// lane.  LDS slot: [0, 1284) lane accumulators + counter | [.., kLsHead) virtual-block pad |
-// ad || le64(|ad|) (16-rounded) | ct (64-rounded) | le64(n) + zeros.
-constexpr uint32_t kLsHead = 1408;
+// 512-thread workgroup, one 64-byte ChaCha20 block per lane (n <= 16384), and
+// the MAC on one wave per record as an i8 MFMA product (mfma_mac): the slot
+// grid of the PL = 64 geometry (64 k blocks) as 32 rows of 2k blocks, 2k <= 42.
+// LDS slot: [0, kLsHead) power table (2k rows x 48 B), later the transposed
+// product tile (16 rows x 132 B) | ad || le64(|ad|) (16-rounded) | ct (64-rounded) |
+// le64(n) + zeros.
+constexpr uint32_t kLsHead = 2176;
+constexpr uint32_t kLsTileStride = 132;
 __host__ __device__ inline bool ls_eligible(uint32_t n, uint32_t adlen) {
-    return n > 8192u && n <= 16384u && (adlen + 16u + n + 15u) / 16u <= 256u * 5u;
+    return n > 8192u && n <= 16384u && (adlen + 16u + n + 15u) / 16u <= 64u * 21u;
 }
 __host__ __device__ inline uint32_t lds_ls_rec_bytes(uint32_t adlen, uint32_t n) {
     return kLsHead + ((adlen + 8u + 15u) & ~15u) + ((n + 63u) & ~63u) + 64u;

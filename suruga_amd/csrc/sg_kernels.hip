@@ -395,15 +395,35 @@ __device__ __forceinline__ uint32_t record_len(const KParams& p, uint32_t rec) {
 // conflicts) and leave as one contiguous 24 KiB run of 16-byte stores; one
 // lane writing its own 384-byte record would touch 64 cache lines per store.
 constexpr uint32_t kKeyingThreads = 64;
-constexpr uint32_t kKeyLdsStride = kKeyRecWords + 1;
 
-template <bool OPEN>
+// sum_{e=1..m} x^e by binary doubling (G(2a) = G(a) + x^a G(a), G(a+1) = G(a) + x^(a+1))
+__device__ __forceinline__ F26 geo_sum(const F26 x, const uint32_t m) {
+    F26 g = f26_zero(), pw = F26{1u, 0u, 0u, 0u, 0u};
+    if (m == 0u) return g;
+    for (int bit = 31 - __builtin_clz(m); bit >= 0; --bit) {
+        g = mul_add(g, pw.v0, pw.v1, pw.v2, pw.v3, pw.v4, g);
+        pw = mul_add(pw, pw.v0, pw.v1, pw.v2, pw.v3, pw.v4, f26_zero());
+        if ((m >> bit) & 1u) {
+            pw = mul_add(pw, x.v0, x.v1, x.v2, x.v3, x.v4, f26_zero());
+            g = F26{g.v0 + pw.v0, g.v1 + pw.v1, g.v2 + pw.v2, g.v3 + pw.v3, g.v4 + pw.v4};
+        }
+    }
+    return g;
+}
+
+template <bool OPEN, bool LS>
 __global__ __launch_bounds__(64) void sg_keying_kernel(const KParams p) {
+    // words [0, kRSmallOff) go through LDS; the lock-step extras (LS) are
+    // written straight from the lane, so the stage stays small (occupancy)
+    constexpr uint32_t RW = LS ? kKeyRecWordsLs : kKeyRecWords;
+    constexpr uint32_t SW = LS ? kRSmallOff : kKeyRecWords;  // staged words per record
+    constexpr uint32_t kKeyLdsStride = SW + 1;
     __shared__ uint32_t stage[kKeyingThreads * kKeyLdsStride];
     const uint32_t lane = threadIdx.x;
     const uint32_t rec0 = blockIdx.x * kKeyingThreads;
     const uint32_t rec = rec0 + lane;
     uint32_t* out = stage + lane * kKeyLdsStride;
+    uint32_t* gout = p.ws + (uint64_t)rec * RW;
     if (rec < p.count) {
         const uint32_t len = record_len(p, rec);
         const uint32_t n = OPEN ? (len >= 16u ? len - 16u : 0u) : len;
@@ -424,7 +444,8 @@ __global__ __launch_bounds__(64) void sg_keying_kernel(const KParams p) {
         // R = r^k by square-and-multiply; then R^0..R^7 and R^0, R^8, .., R^56.
         // mul_add outputs are valid multipliers as they stand (limb 1 may exceed
         // 2^26 by < 2^8), so no extra carry passes are needed here.
-        const MacGeom g = mac_geom(p.tls ? 13u : p.ad_len, n, p.ls ? 256u : mac_lanes(n));
+        const uint32_t adlen = p.tls ? 13u : p.ad_len;
+        const MacGeom g = mac_geom(adlen, n, LS ? 64u : mac_lanes(n));
         const F26 r = words_to_f26(r0, r1, r2, r3, 0u);
         F26 R = r;
         for (int bit = 30 - __builtin_clz(g.k); bit >= 0; --bit) {
@@ -442,25 +463,61 @@ __global__ __launch_bounds__(64) void sg_keying_kernel(const KParams p) {
             store_f26(out + kPowHiOff + 5 * i, x);
             if (i < 7) x = mul_add(x, R8.v0, R8.v1, R8.v2, R8.v3, R8.v4, f26_zero());
         }
-        if (p.ls) {  // wave factors of the lock-step kernel: R^192, R^128, R^64
-            const F26 R64 = mul_add(x, R8.v0, R8.v1, R8.v2, R8.v3, R8.v4, f26_zero());
-            const F26 R128 = mul_add(R64, R64.v0, R64.v1, R64.v2, R64.v3, R64.v4, f26_zero());
-            const F26 R192 = mul_add(R128, R64.v0, R64.v1, R64.v2, R64.v3, R64.v4, f26_zero());
-            store_f26(out + kWavePowOff + 0, R192);
-            store_f26(out + kWavePowOff + 5, R128);
-            store_f26(out + kWavePowOff + 10, R64);
+        if constexpr (LS) {
+            // small powers of r for the MFMA power table (mfma_mac)
+            x = F26{1u, 0u, 0u, 0u, 0u};
+            for (int j = 0; j < 8; ++j) {  // rs[j] = r^j
+                store_f26(gout + kRSmallOff + 5 * j, x);
+                x = mul_add(x, r.v0, r.v1, r.v2, r.v3, r.v4, f26_zero());
+            }
+            const F26 r8 = x;
+            x = F26{1u, 0u, 0u, 0u, 0u};
+            for (int i = 0; i < 6; ++i) {  // rm[i] = r^(8 i)
+                store_f26(gout + kRMidOff + 5 * i, x);
+                if (i < 5) x = mul_add(x, r8.v0, r8.v1, r8.v2, r8.v3, r8.v4, f26_zero());
+            }
+            // Constant term (mfma_mac): with N = 64 k slots, K = 0x80 x 16 bytes
+            // (the i8 bias of the block bytes), J = sum_c 2^(24 + 8 c) (the bias of
+            // the 32 product columns) and H = sum_{u<32} r^(2k u):
+            //   ctot = K G(N) + 2^128 G(B) + [rem < 16] (2^(8 rem) - 2^128) r - J H
+            const uint32_t N = 64u * g.k;
+            const uint32_t rem = g.L - 16u * (g.B - 1u);
+            const F26 R2 = mul_add(R, R.v0, R.v1, R.v2, R.v3, R.v4, f26_zero());
+            F26 H = F26{R2.v0 + 1u, R2.v1, R2.v2, R2.v3, R2.v4}, t = R2;  // (1 + t)(1 + t^2)..(1 + t^16)
+            for (int i = 0; i < 4; ++i) {
+                t = mul_add(t, t.v0, t.v1, t.v2, t.v3, t.v4, f26_zero());
+                H = mul_add(H, t.v0 + 1u, t.v1, t.v2, t.v3, t.v4, f26_zero());
+            }
+            const F26 G2k = geo_sum(r, 2u * g.k);
+            const F26 GN = mul_add(G2k, H.v0, H.v1, H.v2, H.v3, H.v4, f26_zero());  // G(N) = G(2k) H
+            const F26 GB = geo_sum(r, g.B);
+            (void)N;
+            F26 c = mul_add(GN, 0x808080u, 0x202020u, 0x80808u, 0x2020202u, 0x808080u, f26_zero());  // K G(N)
+            c = mul_add(GB, 0u, 0u, 0u, 0u, 0x1000000u, c);                                      // 2^128 G(B)
+            c = mul_add(H, 0x1bd2d2bu, 0x36f6f6fu, 0x3dbdbdbu, 0x2f6f6f6u, 0x1bdbdbdu, c);          // (p - J) H
+            if (rem < 16u) {  // (2^(8 rem) + p - 2^128) r
+                F26 cf = F26{0x3fffffbu, 0x3ffffffu, 0x3ffffffu, 0x3ffffffu, 0x2ffffffu};
+                const uint32_t bit = 8u * rem, li = bit / 26u, v = 1u << (bit - 26u * li);
+                cf.v0 += li == 0u ? v : 0u;
+                cf.v1 += li == 1u ? v : 0u;
+                cf.v2 += li == 2u ? v : 0u;
+                cf.v3 += li == 3u ? v : 0u;
+                cf.v4 += li == 4u ? v : 0u;
+                c = mul_add(cf, r.v0, r.v1, r.v2, r.v3, r.v4, c);
+            }
+            store_f26(gout + kCtotOff, c);
         }
     }
     __syncthreads();
     // coalesced flush: the wave's records are contiguous in the workspace
     const uint32_t nrec = p.count - rec0 < kKeyingThreads ? p.count - rec0 : kKeyingThreads;
-    u32x4* dst = reinterpret_cast<u32x4*>(p.ws + (uint64_t)rec0 * kKeyRecWords);
-    const uint32_t nvec = nrec * (kKeyRecWords / 4u);
+    u32x4* dst = reinterpret_cast<u32x4*>(p.ws + (uint64_t)rec0 * RW);
+    const uint32_t nvec = nrec * (SW / 4u);
     for (uint32_t v = lane; v < nvec; v += kKeyingThreads) {
         const uint32_t w = 4u * v;
-        const uint32_t rr = w / kKeyRecWords, c = w - rr * kKeyRecWords;
+        const uint32_t rr = w / SW, c = w - rr * SW;
         const uint32_t* src = stage + rr * kKeyLdsStride + c;
-        dst[v] = u32x4{src[0], src[1], src[2], src[3]};
+        dst[(rr * RW + c) / 4u] = u32x4{src[0], src[1], src[2], src[3]};
     }
 }
 
@@ -809,150 +866,245 @@ __global__ __launch_bounds__(256) void sg_aead_list_kernel(const KParams p, cons
 //   grouped rounds of sg_chacha_grp.inc -- four adds, four xors, four rotates,
 //   s_barrier -- which keep the two waves of a SIMD in lock-step so that
 //   their full-rate add/xor pair (2 cycles instead of 4);
-// * Poly1305 runs on all 256 lanes (k <= 5 blocks each instead of 17 on one
-//   wave), so no wave carries a long MAC tail that holds the record's LDS:
-//   lane t = 64 w + l scales its Horner sum by R^(64 (3 - w)) (R = r^k) and
-//   adds it into a per-lane LDS accumulator; the last wave scales acc[l] by
-//   R^(63 - l) and sums the lanes with DPP.
-// Measured (profiles/r01_lockstep_ab.md): the rounds run 2.2 ms faster than
-// compiled ones, but the 256-lane MAC costs more than v9's one-wave MAC, so
-// the kernel is 3-5 % slower than sg_aead_kernel on C1: off by default
-// (sg_set_lockstep).
+// * Poly1305 runs on one wave per record as an i8 MFMA product (mfma_mac:
+//   17 v_mfma_i32_32x32x32_i8 for a 16 KiB record, ~300 VALU instead of the
+//   ~870 of v9's Horner MAC or ~1100 of the earlier 256-lane form).
+// Measured (profiles/r01_mfma_mac_ab.md): seal 10.1 ms / open 9.6 ms against
+// v9's 9.75 / 9.70; the MAC's LDS operand loads queue behind the lock-step
+// data path and its one-wave tail holds the workgroup's LDS, so the kernel is
+// off by default (sg_set_lockstep).
 // Seal: load -> rounds -> ct into LDS -> store + MAC.  Open: load -> MAC over
 // the received ciphertext -> rounds -> plaintext -> store (the reference
 // decrypts unconditionally, chacha20_poly1305.rs:80-82).  Every wave runs the
 // same rounds and barriers whatever its record holds: an inactive slot runs
 // on dummy state.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ F26 wave_sum_to_lane63(F26 f) {
-    auto level = [&](auto dpp) {
-        f.v0 += dpp(f.v0); f.v1 += dpp(f.v1); f.v2 += dpp(f.v2); f.v3 += dpp(f.v3); f.v4 += dpp(f.v4);
-    };
-    auto carry = [&]() {
-        uint32_t c;
-        c = f.v0 >> 26; f.v0 &= M26; f.v1 += c;
-        c = f.v1 >> 26; f.v1 &= M26; f.v2 += c;
-        c = f.v2 >> 26; f.v2 &= M26; f.v3 += c;
-        c = f.v3 >> 26; f.v3 &= M26; f.v4 += c;
-        c = f.v4 >> 26; f.v4 &= M26; f.v0 += c * 5u;
-    };
-    // row_shr:1,2,4,8 then row_bcast:15 and row_bcast:31 (see aead_record)
-    level([](uint32_t x) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, true); });
-    level([](uint32_t x) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, true); });
-    level([](uint32_t x) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, true); });
-    level([](uint32_t x) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, true); });
-    level([](uint32_t x) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xf, 0xf, true); });
-    carry();
-    level([](uint32_t x) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xf, 0xf, true); });
-    return f;
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x16 __attribute__((ext_vector_type(16)));
+
+// LDS writes of one lane visible to the other lanes of its wave (and no
+// compiler reordering across it)
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
-// Poly1305 on all 256 lanes of a record: lane t = 64 w + l runs the Horner
-// chain of its k blocks and adds h_t R^(64 (3 - w)) into acc[l]; ls_finish
-// then forms sum_l acc[l] R^(63 - l) = sum_t h_t R^(255 - t).  Exactly the virtual-block scheme of aead_record with
-// PL = 256 (the keying kernel derives k with the same PL when p.ls is set).
-__device__ __forceinline__ void ls_mac(const KParams& p, const uint32_t rec, const uint32_t n, const uint32_t adlen,
-                                       const uint8_t* slot, const uint32_t S, const uint32_t t, const uint32_t w,
-                                       uint32_t* acc) {
-    const uint32_t lane = t & 63u;
-    const MacGeom g = mac_geom(adlen, n, 256u);
-    const uint32_t* kr = p.ws + (uint64_t)rec * kKeyRecWords;
-    const uint32_t r0 = uniform(kr[kR32Off + 0]), r1 = uniform(kr[kR32Off + 1]);
-    const uint32_t r2 = uniform(kr[kR32Off + 2]), r3 = uniform(kr[kR32Off + 3]);
-    const uint32_t s1 = r1 + (r1 >> 2), s2 = r2 + (r2 >> 2), s3 = r3 + (r3 >> 2);
-    const uint32_t v0 = t * g.k;
-    const uint32_t tp = g.z / g.k, nv = g.z - tp * g.k;
-    const uint32_t rem = g.L - 16u * (g.B - 1u);
-    // lanes t < tp hold only virtual blocks (read anything, discarded); lane
-    // tp reads nv virtual blocks in front of the stream (kLsHead leaves room)
-    const uint8_t* blk = t < tp ? slot + S : (t == tp ? slot + S - 16u * nv : slot + S + 16u * (v0 - g.z));
-    H32 h = {0u, 0u, 0u, 0u, 0u};
-    u32x4 m = ldu16(blk);
-    uint32_t j = 0;
-    auto run = [&](const uint32_t e) {
-        for (; j + 2u <= e; j += 2u) {
-            const u32x4 ma = ldu16(blk + 16u * (j + 1u));
-            __builtin_amdgcn_sched_barrier(0);
-            horner_step(h, m.x, m.y, m.z, m.w, 1u, r0, r1, r2, r3, s1, s2, s3);
-            m = ldu16(blk + 16u * (j + 2u));
-            __builtin_amdgcn_sched_barrier(0);
-            horner_step(h, ma.x, ma.y, ma.z, ma.w, 1u, r0, r1, r2, r3, s1, s2, s3);
-        }
-        if (j < e) {
-            const u32x4 mn = ldu16(blk + 16u * (j + 1u));
-            __builtin_amdgcn_sched_barrier(0);
-            horner_step(h, m.x, m.y, m.z, m.w, 1u, r0, r1, r2, r3, s1, s2, s3);
-            m = mn;
-            ++j;
-        }
-    };
-    run(nv);
-    if (t == tp) h = H32{0u, 0u, 0u, 0u, 0u};
-    run(g.k - 1u);
-    uint32_t pad = 1u;
-    if (rem < 16u && t == 255u) {  // partial final block: pad bit at 8 * rem (poly1305.rs:216-225)
-        const uint32_t fb = 1u << (8u * (rem & 3u));
-        const uint32_t fw = rem >> 2;
-        m.x |= fw == 0u ? fb : 0u;
-        m.y |= fw == 1u ? fb : 0u;
-        m.z |= fw == 2u ? fb : 0u;
-        m.w |= fw == 3u ? fb : 0u;
-        pad = 0u;
-    }
-    horner_step(h, m.x, m.y, m.z, m.w, pad, r0, r1, r2, r3, s1, s2, s3);
-    if (t < tp) h = H32{0u, 0u, 0u, 0u, 0u};
-    F26 f = words_to_f26(h.h0, h.h1, h.h2, h.h3, 0u);
-    f.v4 += h.h4 << 24;
-    {
-        const uint32_t c = f.v4 >> 26;
-        f.v4 &= M26;
-        f.v0 += c * 5u;
-    }
-    if (w < 3u) {  // wave factor R^(64 (3 - w))
-        const uint32_t* q = kr + kWavePowOff + 5u * w;
-        f = mul_add(f, uniform(q[0]), uniform(q[1]), uniform(q[2]), uniform(q[3]), uniform(q[4]), f26_zero());
-    }
-    // lane l of every wave shares the factor R^(63 - l): add the four waves'
-    // terms first (LDS atomics, limbs < 2^27 each), scale once (ls_finish)
-    uint32_t* a = acc + 5u * lane;
-    __hip_atomic_fetch_add(a + 0, f.v0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    __hip_atomic_fetch_add(a + 1, f.v1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    __hip_atomic_fetch_add(a + 2, f.v2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    __hip_atomic_fetch_add(a + 3, f.v3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    __hip_atomic_fetch_add(a + 4, f.v4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-// sum_l acc[l] R^(63 - l) + s -> tag; seal appends it (chacha20_poly1305.rs:55),
-// open compares all 16 bytes (:84-93) and writes the record status.
+// Poly1305 of one record on one wave as an i8 MFMA product.
+//
+// The reference evaluates h = sum_j v_j r^(B - j) by Horner's rule
+// (poly1305.rs:213-228), v_j = block j + pad bit.  Take the slot grid of the
+// PL = 64 geometry (mac_geom: N = 64 k slots, the first z virtual and zero)
+// as 32 rows of 2k blocks: slot i = 2k q + s has weight r^(N - i) =
+// W_q P_s with W_q = r^(2k (31 - q)) = R^(62 - 2q) (R = r^k, keying tables)
+// and P_s = r^(2k - s).  Writing P_s in signed base-256 digits P_s[0..16],
+// the byte convolution of a row
+//   S[q][c] = sum_s sum_a (b_{q,s,a} - 128) P_s[c - a],   c = 0..31
+// is one 32 x 32 x (32 k) i8 matrix product: A = the stream bytes with the
+// top bit flipped (row q, K = (s, a)), B = the Toeplitz matrix of the
+// digits (K = (s, a), column c), k MFMA 32x32x32 steps.  |S| < 2^24, so
+// with the accumulator seeded at 2^24 every entry is a positive 25-bit
+// integer and X_q = sum_c S[q][c] 2^(8c) is assembled exactly in radix 2^32.
+// Then h = sum_q W_q X_q + ctot (mod p), where ctot (keying kernel) restores
+// the i8 bias, the 2^24 seed and the pad bits.  Every step is exact integer
+// arithmetic mod 2^130 - 5, so the tag equals the reference's.
 template <bool OPEN>
-__device__ __forceinline__ void ls_finish(const KParams& p, const uint32_t rec, const uint32_t n, const uint8_t* in,
-                                          uint8_t* out, const uint32_t* acc, const uint32_t lane) {
-    const uint32_t* kr = p.ws + (uint64_t)rec * kKeyRecWords;
-    F26 f = load_f26(acc + 5u * lane);
-    {  // limbs < 2^28 here: one carry pass before they enter mul_add
+__device__ __forceinline__ void mfma_mac(const KParams& p, const uint32_t rec, const uint32_t n, const uint32_t adlen,
+                                         uint8_t* slot, const uint32_t S, const uint8_t* in, uint8_t* out,
+                                         const uint32_t lane) {
+#ifndef SG_MAC_PRIO
+#define SG_MAC_PRIO 0
+#endif
+#ifndef SG_MACX
+#define SG_MACX 0  // timing experiments only: stop the MAC after stage 1 (power table), 2 (MFMA), 3 (transpose)
+#endif
+    // The MAC wave runs beside other workgroups' lock-step rounds on its SIMD;
+    // at equal priority its latency chain stretches and holds the record's LDS
+    if (SG_MAC_PRIO) __builtin_amdgcn_s_setprio(SG_MAC_PRIO);
+    const MacGeom g = mac_geom(adlen, n, 64u);
+    const uint32_t rows = 2u * g.k;
+    const uint32_t* kr = p.ws + (uint64_t)rec * kKeyRecWordsLs;
+    // every global operand of the combine is fetched now, so its latency hides
+    // behind the power table and the matrix product: W_q = R^(62 - 2q) = hi[e >> 3] lo[e & 7]
+    const uint32_t we = 62u - 2u * (lane & 31u);
+    const F26 plo = load_f26(kr + kPowLoOff + 5u * (we & 7u));
+    const F26 phi = load_f26(kr + kPowHiOff + 5u * (we >> 3));
+    const F26 ctot = {uniform(kr[kCtotOff + 0]), uniform(kr[kCtotOff + 1]), uniform(kr[kCtotOff + 2]),
+                      uniform(kr[kCtotOff + 3]), uniform(kr[kCtotOff + 4])};
+    uint32_t sk[4] = {uniform(kr[kSOff + 0]), uniform(kr[kSOff + 1]), uniform(kr[kSOff + 2]), uniform(kr[kSOff + 3])};
+    uint32_t rx[4] = {0u, 0u, 0u, 0u};
+    if constexpr (OPEN) {  // the received tag, fetched early (lane 0 compares)
+        if (lane == 0u) {
+            const uint8_t* ep = in + n;
+            if ((((uintptr_t)ep) & 3u) == 0u) {
+                const uint32_t* e32 = reinterpret_cast<const uint32_t*>(ep);
+                rx[0] = e32[0]; rx[1] = e32[1]; rx[2] = e32[2]; rx[3] = e32[3];
+            } else {
+#pragma unroll
+                for (int i = 0; i < 16; ++i) rx[i >> 2] |= (uint32_t)ep[i] << (8 * (i & 3));
+            }
+        }
+    }
+    // ---- power table: row s = P_s's digits, reversed, at slot + 48 s: the 16
+    // bytes at + 31 - c are P_s[c], P_s[c - 1], .., P_s[c - 15] (0 outside 0..16)
+    if (lane < rows) {
+        const uint32_t e = rows - lane;
+        const F26 pm = load_f26(kr + kRMidOff + 5u * (e >> 3));
+        const F26 ps = load_f26(kr + kRSmallOff + 5u * (e & 7u));
+        const F26 v = canonical(mul_add(pm, ps.v0, ps.v1, ps.v2, ps.v3, ps.v4, f26_zero()));
+        // signed digits of V = the bytes of V + 0x80..80 (17 bytes), each minus 0x80
+        uint32_t c;
+        const uint32_t w0 = addc(v.v0 | (v.v1 << 26), 0x80808080u, 0u, &c);
+        const uint32_t w1 = addc((v.v1 >> 6) | (v.v2 << 20), 0x80808080u, c, &c);
+        const uint32_t w2 = addc((v.v2 >> 12) | (v.v3 << 14), 0x80808080u, c, &c);
+        const uint32_t w3 = addc((v.v3 >> 18) | (v.v4 << 8), 0x80808080u, c, &c);
+        const uint32_t w4 = (v.v4 >> 24) + 0x80u + c;
+        uint8_t* F = slot + 48u * lane;
+        st16(F, u32x4{0u, 0u, 0u, ((w4 ^ 0x80u) & 0xffu) << 24});
+        st16(F + 16, u32x4{bswap32(w3 ^ 0x80808080u), bswap32(w2 ^ 0x80808080u), bswap32(w1 ^ 0x80808080u),
+                           bswap32(w0 ^ 0x80808080u)});
+        st16(F + 32, u32x4{0u, 0u, 0u, 0u});
+    }
+    wave_lds_sync();
+    if (SG_MACX == 1) return;
+    // ---- S = A B on the matrix cores: lane = (half h, row/column q) ----------
+    const uint32_t q = lane & 31u, hh = lane >> 5;
+    const uint32_t zoff = S + adlen + 8u + n + 8u;  // 16 zero bytes behind le64(n): the virtual blocks
+    i32x16 acc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 1 << 24;
+    auto a_at = [&](const uint32_t i) {
+        const uint32_t si = rows * q + 2u * i + hh;
+        const uint32_t o = si < g.z ? zoff : S + 16u * (si - g.z);
+        return slot + ((SG_MACX == 6 || SG_MACX == 8) ? (o & ~15u) : o);  // 6, 8: timing experiments, aligned A
+    };
+    auto b_at = [&](const uint32_t i) {
+        const uint32_t o = 48u * (2u * i + hh) + 31u - q;
+        return slot + ((SG_MACX == 7 || SG_MACX == 8) ? (o & ~15u) : o);  // 7, 8: timing experiments, aligned B
+    };
+    // operands of step i + 1 are loaded while step i runs
+    u32x4 a = ldu16(a_at(0)), b = ldu16(b_at(0));
+#if SG_MACX == 4  // experiment: the products without the LDS operand loads
+    for (uint32_t i = 0; i < g.k; ++i) {
+        acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(__builtin_bit_cast(i32x4, a ^ i),
+                                                     __builtin_bit_cast(i32x4, b), acc, 0, 0, 0);
+    }
+#elif SG_MACX == 5  // experiment: the LDS operand loads without the products
+    for (uint32_t i = 0; i < g.k; ++i) {
+        const uint32_t nx = i + 1u < g.k ? i + 1u : i;
+        const u32x4 an = ldu16(a_at(nx)), bn = ldu16(b_at(nx));
+        acc[i & 15] += (int)(a.x ^ b.y ^ a.w ^ b.z);
+        a = an;
+        b = bn;
+    }
+#else
+    for (uint32_t i = 0; i < g.k; ++i) {
+        const uint32_t nx = i + 1u < g.k ? i + 1u : i;
+        const u32x4 an = ldu16(a_at(nx)), bn = ldu16(b_at(nx));
+        acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(__builtin_bit_cast(i32x4, a ^ 0x80808080u),
+                                                     __builtin_bit_cast(i32x4, b), acc, 0, 0, 0);
+        a = an;
+        b = bn;
+    }
+#endif
+    // ---- transpose through LDS (over the power table), 16 rows at a time:
+    // accumulator i of lane (h, q) is S[(i & 3) + 8 (i >> 2) + 4 h][q]; lane q' < 32 takes row q'
+    if (SG_MACX == 2 || SG_MACX == 4 || SG_MACX == 5) {
+        if (lane == 0 && acc[0] == 12345 && acc[15] == 54321) p.status[rec] = 7;  // keep the product live
+        return;
+    }
+    uint32_t X[32];
+    wave_lds_sync();
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int i = 8 * pass + j;
+            const uint32_t row = (uint32_t)((i & 3) + 8 * (i >> 2) - 16 * pass) + 4u * hh;
+            *reinterpret_cast<int*>(slot + kLsTileStride * row + 4u * q) = acc[i];
+        }
+        wave_lds_sync();
+        if ((lane >> 4) == (uint32_t)pass) {
+            const uint8_t* rp = slot + kLsTileStride * (lane & 15u);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const u32x4 v = ldu16(rp + 16 * j);
+                X[4 * j] = v.x; X[4 * j + 1] = v.y; X[4 * j + 2] = v.z; X[4 * j + 3] = v.w;
+            }
+        }
+        wave_lds_sync();
+    }
+    if (SG_MACX == 3) {
+        if (lane == 0 && X[0] == 12345 && X[31] == 54321) p.status[rec] = 7;
+        return;
+    }
+    // ---- X_q = sum_c S'[q][c] 2^(8c) (radix 2^32, 9 words): the four byte
+    // phases c = 4m + j are each a run of non-overlapping 25-bit words
+    uint32_t wv[9];
+    {
+        uint32_t c1 = 0u, c2 = 0u, c3 = 0u;
+#pragma unroll
+        for (int m = 0; m < 9; ++m) {
+            const uint32_t t0 = m < 8 ? X[4 * m] : 0u;
+            const uint32_t t1 = __builtin_amdgcn_alignbit(m < 8 ? X[4 * m + 1] : 0u, m > 0 ? X[4 * m - 3] : 0u, 24);
+            const uint32_t t2 = __builtin_amdgcn_alignbit(m < 8 ? X[4 * m + 2] : 0u, m > 0 ? X[4 * m - 2] : 0u, 16);
+            const uint32_t t3 = __builtin_amdgcn_alignbit(m < 8 ? X[4 * m + 3] : 0u, m > 0 ? X[4 * m - 1] : 0u, 8);
+            uint32_t x = addc(t0, t1, c1, &c1);
+            x = addc(x, t2, c2, &c2);
+            wv[m] = addc(x, t3, c3, &c3);
+        }
+    }
+    // ---- mod p: fold everything from 2^130 up twice (2^130 == 5 mod p)
+    F26 f;
+    {
+        uint64_t t = (uint64_t)__builtin_amdgcn_alignbit(wv[5], wv[4], 2) * 5u + wv[0];
+        const uint32_t y0 = (uint32_t)t;
+        t = (uint64_t)__builtin_amdgcn_alignbit(wv[6], wv[5], 2) * 5u + wv[1] + (t >> 32);
+        const uint32_t y1 = (uint32_t)t;
+        t = (uint64_t)__builtin_amdgcn_alignbit(wv[7], wv[6], 2) * 5u + wv[2] + (t >> 32);
+        const uint32_t y2 = (uint32_t)t;
+        t = (uint64_t)__builtin_amdgcn_alignbit(wv[8], wv[7], 2) * 5u + wv[3] + (t >> 32);
+        const uint32_t y3 = (uint32_t)t;
+        t = (uint64_t)(wv[8] >> 2) * 5u + (wv[4] & 3u) + (t >> 32);  // y = y0..y3 + t 2^128 < 2^162
+        const uint64_t u = (uint64_t)(uint32_t)(t >> 2) * 5u + y0;   // (y mod 2^130) + 5 (y >> 130)
+        uint32_t c;
+        const uint32_t z1 = addc(y1, (uint32_t)(u >> 32), 0u, &c);
+        const uint32_t z2 = addc(y2, 0u, c, &c);
+        const uint32_t z3 = addc(y3, 0u, c, &c);
+        const uint32_t z4 = ((uint32_t)t & 3u) + c;  // <= 4
+        f = words_to_f26((uint32_t)u, z1, z2, z3, 0u);
+        f.v4 += z4 << 24;
+    }
+    {  // * W_q
+        f = mul_add(f, plo.v0, plo.v1, plo.v2, plo.v3, plo.v4, f26_zero());
+        f = mul_add(f, phi.v0, phi.v1, phi.v2, phi.v3, phi.v4, f26_zero());
+    }
+    if (lane >= 32u) f = f26_zero();
+    {  // sum lanes 0..31 into lane 31: row_shr 1, 2, 4, 8, then row_bcast:15
+        auto level = [&](auto dpp) {
+            f.v0 += dpp(f.v0); f.v1 += dpp(f.v1); f.v2 += dpp(f.v2); f.v3 += dpp(f.v3); f.v4 += dpp(f.v4);
+        };
+        level([](uint32_t x) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, true); });
+        level([](uint32_t x) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, true); });
+        level([](uint32_t x) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, true); });
+        level([](uint32_t x) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, true); });
         uint32_t c;
         c = f.v0 >> 26; f.v0 &= M26; f.v1 += c;
         c = f.v1 >> 26; f.v1 &= M26; f.v2 += c;
         c = f.v2 >> 26; f.v2 &= M26; f.v3 += c;
         c = f.v3 >> 26; f.v3 &= M26; f.v4 += c;
         c = f.v4 >> 26; f.v4 &= M26; f.v0 += c * 5u;
+        level([](uint32_t x) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xf, 0xf, true); });
     }
-    {  // lane factor R^(63 - lane) = hi[e >> 3] lo[e & 7]
-        const uint32_t e = 63u - lane;
-        const F26 plo = load_f26(kr + kPowLoOff + 5u * (e & 7u));
-        const F26 phi = load_f26(kr + kPowHiOff + 5u * (e >> 3));
-        const F26 P = mul_add(phi, plo.v0, plo.v1, plo.v2, plo.v3, plo.v4, f26_zero());
-        f = mul_add(f, P.v0, P.v1, P.v2, P.v3, P.v4, f26_zero());
-    }
-    f = wave_sum_to_lane63(f);
-    auto lane63 = [](uint32_t x) { return (uint32_t)__builtin_amdgcn_readlane((int)x, 63); };
-    f = F26{lane63(f.v0), lane63(f.v1), lane63(f.v2), lane63(f.v3), lane63(f.v4)};
-    uint32_t s[4] = {uniform(kr[kSOff + 0]), uniform(kr[kSOff + 1]), uniform(kr[kSOff + 2]), uniform(kr[kSOff + 3])};
+    // the sum leaves lane 31 for SGPRs: + ctot, canonical residue, + s (poly1305.rs:231-312)
+    auto lane31 = [](uint32_t x) { return (uint32_t)__builtin_amdgcn_readlane((int)x, 31); };
+    const F26 fs = {lane31(f.v0) + ctot.v0, lane31(f.v1) + ctot.v1, lane31(f.v2) + ctot.v2, lane31(f.v3) + ctot.v3,
+                    lane31(f.v4) + ctot.v4};
     uint32_t tw[4];
-    tag_words(f, s, tw);
+    tag_words(fs, sk, tw);
     if (lane != 0u) return;
     if constexpr (!OPEN) {
-        uint8_t* tp = out + n;
+        uint8_t* tp = out + n;  // ct || tag (chacha20_poly1305.rs:55)
         if ((((uintptr_t)tp) & 3u) == 0u) {
             uint32_t* t32 = reinterpret_cast<uint32_t*>(tp);
             t32[0] = tw[0]; t32[1] = tw[1]; t32[2] = tw[2]; t32[3] = tw[3];
@@ -961,15 +1113,7 @@ __device__ __forceinline__ void ls_finish(const KParams& p, const uint32_t rec, 
             for (int i = 0; i < 16; ++i) tp[i] = (uint8_t)(tw[i >> 2] >> (8 * (i & 3)));
         }
     } else {
-        uint32_t rx[4] = {0u, 0u, 0u, 0u};
-        const uint8_t* ep = in + n;
-        if ((((uintptr_t)ep) & 3u) == 0u) {
-            const uint32_t* e32 = reinterpret_cast<const uint32_t*>(ep);
-            rx[0] = e32[0]; rx[1] = e32[1]; rx[2] = e32[2]; rx[3] = e32[3];
-        } else {
-#pragma unroll
-            for (int i = 0; i < 16; ++i) rx[i >> 2] |= (uint32_t)ep[i] << (8 * (i & 3));
-        }
+        // constant-time compare: diff |= a ^ b over all 16 bytes (chacha20_poly1305.rs:84-87)
         const uint32_t diff = (rx[0] ^ tw[0]) | (rx[1] ^ tw[1]) | (rx[2] ^ tw[2]) | (rx[3] ^ tw[3]);
         p.status[rec] = diff != 0u ? 1u : 0u;
     }
@@ -994,7 +1138,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
     const uint32_t rec = blockIdx.x * 2u + g;
     const bool active = rec < p.count;
     uint8_t* slot = lds + g * p.lds_rec_bytes;
-    uint32_t* acc = reinterpret_cast<uint32_t*>(slot);  // [64][5] lane accumulators, then the arrival counter
     const uint32_t n = OPEN ? p.uniform_len - 16u : p.uniform_len;
     const uint32_t adlen = p.tls ? 13u : p.ad_len;
     const uint32_t A = kLsHead + ((adlen + 8u + 15u) & ~15u);
@@ -1007,8 +1150,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
         in = p.in + (p.in_off ? p.in_off[rec] : p.in_stride * rec);
         out = p.out + (p.out_off ? p.out_off[rec] : p.out_stride * rec);
         rk = record_key(p, rec);
-        acc[t] = 0u;
-        if (t < 65u) acc[256u + t] = 0u;  // the rest of acc and the arrival counter acc[320]
         // ---- the record into LDS, lane-contiguous ----
         const uint32_t tail = n & ~15u;
         if ((((uintptr_t)in) & 15u) == 0u) {
@@ -1037,7 +1178,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
     }
     __syncthreads();
     if constexpr (OPEN) {
-        if (active && !SG_LS_NOMAC) ls_mac(p, rec, n, adlen, slot, S, t, w, acc);
+        // one wave per record (spread over the SIMDs) runs the MAC over the received ciphertext
+        if (active && w == (rec & 3u) && !SG_LS_NOMAC) mfma_mac<true>(p, rec, n, adlen, slot, S, in, out, lane);
         __syncthreads();  // every MAC read is done before the plaintext replaces the ciphertext
     }
     // ---- keystream block t + 1 in lock-step; XOR in LDS ----
@@ -1093,18 +1235,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
         }
     }
     if constexpr (!OPEN) {
-        if (!active || SG_LS_NOMAC) return;
-        ls_mac(p, rec, n, adlen, slot, S, t, w, acc);
-        // the last wave of the record to finish scales and sums the accumulators
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        uint32_t old = 0u;
-        if (lane == 63u) old = __hip_atomic_fetch_add(acc + 320, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
-        old = (uint32_t)__builtin_amdgcn_readlane((int)old, 63);
-        if (old != 3u) return;
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        ls_finish<false>(p, rec, n, in, out, acc, lane);
-    } else {
-        if (active && w == (rec & 3u) && !SG_LS_NOMAC) ls_finish<true>(p, rec, n, in, out, acc, lane);
+        if (active && w == (rec & 3u) && !SG_LS_NOMAC) mfma_mac<false>(p, rec, n, adlen, slot, S, in, out, lane);
     }
 }
 
@@ -1222,10 +1353,16 @@ __global__ __launch_bounds__(256) void sg_compare_kernel(const uint8_t* a, uint6
 
 hipError_t launch_keying(const KParams& p, bool open, hipStream_t s) {
     const uint32_t grid = (p.count + kKeyingThreads - 1u) / kKeyingThreads;
-    if (open)
-        hipLaunchKernelGGL(sg_keying_kernel<true>, dim3(grid), dim3(kKeyingThreads), 0, s, p);
-    else
-        hipLaunchKernelGGL(sg_keying_kernel<false>, dim3(grid), dim3(kKeyingThreads), 0, s, p);
+    if (p.ls) {
+        if (open)
+            hipLaunchKernelGGL((sg_keying_kernel<true, true>), dim3(grid), dim3(kKeyingThreads), 0, s, p);
+        else
+            hipLaunchKernelGGL((sg_keying_kernel<false, true>), dim3(grid), dim3(kKeyingThreads), 0, s, p);
+    } else if (open) {
+        hipLaunchKernelGGL((sg_keying_kernel<true, false>), dim3(grid), dim3(kKeyingThreads), 0, s, p);
+    } else {
+        hipLaunchKernelGGL((sg_keying_kernel<false, false>), dim3(grid), dim3(kKeyingThreads), 0, s, p);
+    }
     return hipGetLastError();
 }
 
@@ -1364,11 +1501,12 @@ const char* kernel_config() {
 #define SG_STR2(x) #x
 #define SG_STR(x) SG_STR2(x)
     if (lockstep_enabled())
-        return "gfx950 sg_aead_kernel v10" "/salu_pre=" SG_STR(SG_SALU_PRE) "/mac_v2=1/lockstep=1"
+        return "gfx950 sg_aead_kernel v11" "/salu_pre=" SG_STR(SG_SALU_PRE) "/mac_v2=1/lockstep=1"
                ": uniform 8-16 KiB batches on sg_aead_ls_kernel (two records per 512-thread workgroup, lane-contiguous "
-               "loads/stores through LDS, grouped lock-step ChaCha20 rounds with s_barrier per rotate group, Poly1305 on "
-               "all 256 lanes: k<=5 blocks per lane, per-wave R^(64(3-w)) scaling into per-lane LDS accumulators, one "
-               "R^(63-lane) scaling + DPP sum); other batches: 8 size classes as v9, keying pre-pass";
+               "loads/stores through LDS, grouped lock-step ChaCha20 rounds with s_barrier per rotate group, Poly1305 as an "
+               "i8 MFMA product on one wave per record: 32 rows x 2k blocks, Toeplitz digit matrix of r^1..r^2k, "
+               "v_mfma_i32_32x32x32_i8, exact row assembly, W_q scaling + DPP sum, keying constant term); other batches: "
+               "8 size classes as v9, keying pre-pass";
     return "gfx950 sg_aead_kernel v9" "/salu_pre=" SG_STR(SG_SALU_PRE) "/mac_v2=1"
            ": 8 size classes (2..256 lanes per record, one 64-B block per lane, device bucketing, exact class grids), "
            "lane=64B ChaCha block (counter-free round-1 QRs on SALU for wave-uniform records), Poly1305 contiguous-chunk "
