@@ -16,18 +16,20 @@ constexpr uint32_t kKeyRecWords = 104;    // per-record keying output (u32 words
 //   hi[8][5] = R^(8 i)   i = 0..7
 // so that MAC lane t = 8a + b scales its partial sum by R^(63-t) = hi[7-a] lo[7-b];
 // The lock-step kernel (KParams::ls, MFMA Poly1305, k from PL = 64 as above)
-// uses a longer record (kKeyRecWordsLs words) that appends, radix 2^26:
-//   rs[8][5]  = r^j        j = 0..7
-//   rm[6][5]  = r^(8 i)    i = 0..5     (r^e = rm[e >> 3] rs[e & 7], e <= 47)
-//   ctot[5]   = the record's constant term of the MFMA evaluation (mfma_mac)
+// uses a longer record (kKeyRecWordsLs words), radix 2^26, in place of lo/hi:
+//   pl[8][5] = r^(32 j + 1)  j = 0..7   (at kPowLoOff)
+//   ph[6][5] = r^(256 i)     i = 0..5   (at kPowHiOff; P_t = r^(32 t + 1) = ph[t >> 3] pl[t & 7])
+//   rs[8][5] = r^j           j = 0..7
+//   rm[4][5] = r^(8 i)       i = 0..3   (W_q = r^(31 - q) = rm[e >> 3] rs[e & 7])
+//   ctot[5]  = the record's constant term of the MFMA evaluation (mfma_mac)
 constexpr uint32_t kR32Off = 0;
 constexpr uint32_t kSOff = 4;
 constexpr uint32_t kPowLoOff = 8;
 constexpr uint32_t kPowHiOff = 48;
 constexpr uint32_t kRSmallOff = 88;
 constexpr uint32_t kRMidOff = 128;
-constexpr uint32_t kCtotOff = 158;
-constexpr uint32_t kKeyRecWordsLs = 164;
+constexpr uint32_t kCtotOff = 148;
+constexpr uint32_t kKeyRecWordsLs = 156;
 constexpr uint32_t kKeyRecWordsMax = kKeyRecWordsLs;
 
 // Kernel parameters (passed by value as kernarg).
@@ -83,7 +85,8 @@ __host__ __device__ inline uint32_t lds_rec_bytes(uint32_t cls, uint32_t adlen, 
 // Lock-step kernel (sg_aead_ls_kernel): two records of one length n per
 // 512-thread workgroup, one 64-byte ChaCha20 block per lane (n <= 16384), and
 // the MAC on one wave per record as an i8 MFMA product (mfma_mac): the slot
-// grid of the PL = 64 geometry (64 k blocks) as 32 rows of 2k blocks, 2k <= 42.
+// grid of the PL = 64 geometry (64 k blocks) as 32 rows (slot 32 s + q in
+// row q) of 2k blocks, 2k <= 42.
 // LDS slot: [0, kLsHead) power table (2k rows x 48 B), later the transposed
 // product tile (16 rows x 132 B) | ad || le64(|ad|) (16-rounded) | ct (64-rounded) |
 // le64(n) + zeros.

@@ -441,60 +441,72 @@ __global__ __launch_bounds__(64) void sg_keying_kernel(const KParams p) {
         out[kSOff + 1] = ks[5];
         out[kSOff + 2] = ks[6];
         out[kSOff + 3] = ks[7];
-        // R = r^k by square-and-multiply; then R^0..R^7 and R^0, R^8, .., R^56.
-        // mul_add outputs are valid multipliers as they stand (limb 1 may exceed
-        // 2^26 by < 2^8), so no extra carry passes are needed here.
         const uint32_t adlen = p.tls ? 13u : p.ad_len;
         const MacGeom g = mac_geom(adlen, n, LS ? 64u : mac_lanes(n));
         const F26 r = words_to_f26(r0, r1, r2, r3, 0u);
-        F26 R = r;
-        for (int bit = 30 - __builtin_clz(g.k); bit >= 0; --bit) {
-            R = mul_add(R, R.v0, R.v1, R.v2, R.v3, R.v4, f26_zero());
-            if ((g.k >> bit) & 1u) R = mul_add(R, r.v0, r.v1, r.v2, r.v3, r.v4, f26_zero());
-        }
-        F26 x = F26{1u, 0u, 0u, 0u, 0u};
-        for (int j = 0; j < 8; ++j) {  // lo[j] = R^j
-            store_f26(out + kPowLoOff + 5 * j, x);
-            x = mul_add(x, R.v0, R.v1, R.v2, R.v3, R.v4, f26_zero());
-        }
-        const F26 R8 = x;
-        x = F26{1u, 0u, 0u, 0u, 0u};
-        for (int i = 0; i < 8; ++i) {  // hi[i] = R^(8 i)
-            store_f26(out + kPowHiOff + 5 * i, x);
-            if (i < 7) x = mul_add(x, R8.v0, R8.v1, R8.v2, R8.v3, R8.v4, f26_zero());
-        }
-        if constexpr (LS) {
-            // small powers of r for the MFMA power table (mfma_mac)
+        if constexpr (!LS) {
+            // R = r^k by square-and-multiply; then R^0..R^7 and R^0, R^8, .., R^56.
+            // mul_add outputs are valid multipliers as they stand (limb 1 may exceed
+            // 2^26 by < 2^8), so no extra carry passes are needed here.
+            F26 R = r;
+            for (int bit = 30 - __builtin_clz(g.k); bit >= 0; --bit) {
+                R = mul_add(R, R.v0, R.v1, R.v2, R.v3, R.v4, f26_zero());
+                if ((g.k >> bit) & 1u) R = mul_add(R, r.v0, r.v1, r.v2, r.v3, r.v4, f26_zero());
+            }
+            F26 x = F26{1u, 0u, 0u, 0u, 0u};
+            for (int j = 0; j < 8; ++j) {  // lo[j] = R^j
+                store_f26(out + kPowLoOff + 5 * j, x);
+                x = mul_add(x, R.v0, R.v1, R.v2, R.v3, R.v4, f26_zero());
+            }
+            const F26 R8 = x;
             x = F26{1u, 0u, 0u, 0u, 0u};
+            for (int i = 0; i < 8; ++i) {  // hi[i] = R^(8 i)
+                store_f26(out + kPowHiOff + 5 * i, x);
+                if (i < 7) x = mul_add(x, R8.v0, R8.v1, R8.v2, R8.v3, R8.v4, f26_zero());
+            }
+        } else {
+            // power tables of the MFMA evaluation (mfma_mac)
+            F26 x = F26{1u, 0u, 0u, 0u, 0u};
             for (int j = 0; j < 8; ++j) {  // rs[j] = r^j
                 store_f26(gout + kRSmallOff + 5 * j, x);
                 x = mul_add(x, r.v0, r.v1, r.v2, r.v3, r.v4, f26_zero());
             }
             const F26 r8 = x;
             x = F26{1u, 0u, 0u, 0u, 0u};
-            for (int i = 0; i < 6; ++i) {  // rm[i] = r^(8 i)
+            for (int i = 0; i < 4; ++i) {  // rm[i] = r^(8 i); x ends at r^32
                 store_f26(gout + kRMidOff + 5 * i, x);
-                if (i < 5) x = mul_add(x, r8.v0, r8.v1, r8.v2, r8.v3, r8.v4, f26_zero());
+                x = mul_add(x, r8.v0, r8.v1, r8.v2, r8.v3, r8.v4, f26_zero());
+            }
+            const F26 r32 = x;
+            x = r;
+            for (int j = 0; j < 8; ++j) {  // pl[j] = r^(32 j + 1)
+                store_f26(out + kPowLoOff + 5 * j, x);
+                x = mul_add(x, r32.v0, r32.v1, r32.v2, r32.v3, r32.v4, f26_zero());
+            }
+            F26 r256 = mul_add(r32, r32.v0, r32.v1, r32.v2, r32.v3, r32.v4, f26_zero());
+            r256 = mul_add(r256, r256.v0, r256.v1, r256.v2, r256.v3, r256.v4, f26_zero());
+            r256 = mul_add(r256, r256.v0, r256.v1, r256.v2, r256.v3, r256.v4, f26_zero());
+            x = F26{1u, 0u, 0u, 0u, 0u};
+            for (int i = 0; i < 6; ++i) {  // ph[i] = r^(256 i)
+                store_f26(out + kPowHiOff + 5 * i, x);
+                if (i < 5) x = mul_add(x, r256.v0, r256.v1, r256.v2, r256.v3, r256.v4, f26_zero());
             }
             // Constant term (mfma_mac): with N = 64 k slots, K = 0x80 x 16 bytes
-            // (the i8 bias of the block bytes), J = sum_c 2^(24 + 8 c) (the bias of
-            // the 32 product columns) and H = sum_{u<32} r^(2k u):
-            //   ctot = K G(N) + 2^128 G(B) + [rem < 16] (2^(8 rem) - 2^128) r - J H
-            const uint32_t N = 64u * g.k;
+            // (the i8 bias of the block bytes), J = sum_c 2^(24 + 8 c) (the seed of
+            // the 32 product columns), G(m) = sum_{e=1..m} r^e and the row weights
+            // W_q = r^(31 - q), sum_q W_q = 1 + G(31):
+            //   ctot = K G(N) + 2^128 G(B) + [rem < 16] (2^(8 rem) - 2^128) r - J (1 + G(31))
+            // with G(N) = G(32) sum_{t < 2k} r^(32 t).
             const uint32_t rem = g.L - 16u * (g.B - 1u);
-            const F26 R2 = mul_add(R, R.v0, R.v1, R.v2, R.v3, R.v4, f26_zero());
-            F26 H = F26{R2.v0 + 1u, R2.v1, R2.v2, R2.v3, R2.v4}, t = R2;  // (1 + t)(1 + t^2)..(1 + t^16)
-            for (int i = 0; i < 4; ++i) {
-                t = mul_add(t, t.v0, t.v1, t.v2, t.v3, t.v4, f26_zero());
-                H = mul_add(H, t.v0 + 1u, t.v1, t.v2, t.v3, t.v4, f26_zero());
-            }
-            const F26 G2k = geo_sum(r, 2u * g.k);
-            const F26 GN = mul_add(G2k, H.v0, H.v1, H.v2, H.v3, H.v4, f26_zero());  // G(N) = G(2k) H
+            const F26 G31 = geo_sum(r, 31u);
+            const F26 G32 = F26{G31.v0 + r32.v0, G31.v1 + r32.v1, G31.v2 + r32.v2, G31.v3 + r32.v3, G31.v4 + r32.v4};
+            const F26 T = geo_sum(r32, 2u * g.k - 1u);
+            const F26 GN = mul_add(G32, T.v0 + 1u, T.v1, T.v2, T.v3, T.v4, f26_zero());
             const F26 GB = geo_sum(r, g.B);
-            (void)N;
             F26 c = mul_add(GN, 0x808080u, 0x202020u, 0x80808u, 0x2020202u, 0x808080u, f26_zero());  // K G(N)
             c = mul_add(GB, 0u, 0u, 0u, 0u, 0x1000000u, c);                                      // 2^128 G(B)
-            c = mul_add(H, 0x1bd2d2bu, 0x36f6f6fu, 0x3dbdbdbu, 0x2f6f6f6u, 0x1bdbdbdu, c);          // (p - J) H
+            c = mul_add(F26{G31.v0 + 1u, G31.v1, G31.v2, G31.v3, G31.v4}, 0x1bd2d2bu, 0x36f6f6fu, 0x3dbdbdbu,
+                        0x2f6f6f6u, 0x1bdbdbdu, c);                                                // (p - J)(1 + G(31))
             if (rem < 16u) {  // (2^(8 rem) + p - 2^128) r
                 F26 cf = F26{0x3fffffbu, 0x3ffffffu, 0x3ffffffu, 0x3ffffffu, 0x2ffffffu};
                 const uint32_t bit = 8u * rem, li = bit / 26u, v = 1u << (bit - 26u * li);
@@ -895,10 +907,10 @@ __device__ __forceinline__ void wave_lds_sync() {
 // The reference evaluates h = sum_j v_j r^(B - j) by Horner's rule
 // (poly1305.rs:213-228), v_j = block j + pad bit.  Take the slot grid of the
 // PL = 64 geometry (mac_geom: N = 64 k slots, the first z virtual and zero)
-// as 32 rows of 2k blocks: slot i = 2k q + s has weight r^(N - i) =
-// W_q P_s with W_q = r^(2k (31 - q)) = R^(62 - 2q) (R = r^k, keying tables)
-// and P_s = r^(2k - s).  Writing P_s in signed base-256 digits P_s[0..16],
-// the byte convolution of a row
+// as 32 rows of 2k blocks, slot i = 32 s + q in row q (so the 32 lanes of a
+// half-wave read 32 consecutive blocks): its weight r^(N - i) = W_q P_s with
+// W_q = r^(31 - q) and P_s = r^(32 (2k - 1 - s) + 1) (keying tables).
+// Writing P_s in signed base-256 digits P_s[0..16], the byte convolution of a row
 //   S[q][c] = sum_s sum_a (b_{q,s,a} - 128) P_s[c - a],   c = 0..31
 // is one 32 x 32 x (32 k) i8 matrix product: A = the stream bytes with the
 // top bit flipped (row q, K = (s, a)), B = the Toeplitz matrix of the
@@ -925,10 +937,10 @@ __device__ __forceinline__ void mfma_mac(const KParams& p, const uint32_t rec, c
     const uint32_t rows = 2u * g.k;
     const uint32_t* kr = p.ws + (uint64_t)rec * kKeyRecWordsLs;
     // every global operand of the combine is fetched now, so its latency hides
-    // behind the power table and the matrix product: W_q = R^(62 - 2q) = hi[e >> 3] lo[e & 7]
-    const uint32_t we = 62u - 2u * (lane & 31u);
-    const F26 plo = load_f26(kr + kPowLoOff + 5u * (we & 7u));
-    const F26 phi = load_f26(kr + kPowHiOff + 5u * (we >> 3));
+    // behind the power table and the matrix product: W_q = r^(31 - q) = rm[e >> 3] rs[e & 7]
+    const uint32_t we = 31u - (lane & 31u);
+    const F26 plo = load_f26(kr + kRSmallOff + 5u * (we & 7u));
+    const F26 phi = load_f26(kr + kRMidOff + 5u * (we >> 3));
     const F26 ctot = {uniform(kr[kCtotOff + 0]), uniform(kr[kCtotOff + 1]), uniform(kr[kCtotOff + 2]),
                       uniform(kr[kCtotOff + 3]), uniform(kr[kCtotOff + 4])};
     uint32_t sk[4] = {uniform(kr[kSOff + 0]), uniform(kr[kSOff + 1]), uniform(kr[kSOff + 2]), uniform(kr[kSOff + 3])};
@@ -946,11 +958,12 @@ __device__ __forceinline__ void mfma_mac(const KParams& p, const uint32_t rec, c
         }
     }
     // ---- power table: row s = P_s's digits, reversed, at slot + 48 s: the 16
-    // bytes at + 31 - c are P_s[c], P_s[c - 1], .., P_s[c - 15] (0 outside 0..16)
+    // bytes at + 31 - c are P_s[c], P_s[c - 1], .., P_s[c - 15] (0 outside 0..16);
+    // P_s = r^(32 t + 1), t = 2k - 1 - s
     if (lane < rows) {
-        const uint32_t e = rows - lane;
-        const F26 pm = load_f26(kr + kRMidOff + 5u * (e >> 3));
-        const F26 ps = load_f26(kr + kRSmallOff + 5u * (e & 7u));
+        const uint32_t e = rows - 1u - lane;
+        const F26 pm = load_f26(kr + kPowHiOff + 5u * (e >> 3));
+        const F26 ps = load_f26(kr + kPowLoOff + 5u * (e & 7u));
         const F26 v = canonical(mul_add(pm, ps.v0, ps.v1, ps.v2, ps.v3, ps.v4, f26_zero()));
         // signed digits of V = the bytes of V + 0x80..80 (17 bytes), each minus 0x80
         uint32_t c;
@@ -974,7 +987,7 @@ __device__ __forceinline__ void mfma_mac(const KParams& p, const uint32_t rec, c
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[i] = 1 << 24;
     auto a_at = [&](const uint32_t i) {
-        const uint32_t si = rows * q + 2u * i + hh;
+        const uint32_t si = 32u * (2u * i + hh) + q;  // lanes q read consecutive blocks
         const uint32_t o = si < g.z ? zoff : S + 16u * (si - g.z);
         return slot + ((SG_MACX == 6 || SG_MACX == 8) ? (o & ~15u) : o);  // 6, 8: timing experiments, aligned A
     };
