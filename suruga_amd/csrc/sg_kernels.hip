@@ -995,8 +995,27 @@ __device__ __forceinline__ void mfma_mac(const KParams& p, const uint32_t rec, c
         const uint32_t o = 48u * (2u * i + hh) + 31u - q;
         return slot + ((SG_MACX == 7 || SG_MACX == 8) ? (o & ~15u) : o);  // 7, 8: timing experiments, aligned B
     };
+#ifndef SG_MAC_GLOBAL_A
+#define SG_MAC_GLOBAL_A 0
+#endif
+    // Experiment switch (off): A blocks that lie wholly inside the ciphertext
+    // read from the record in global memory (L2-resident: this workgroup just
+    // stored it (seal) or loaded it (open)) instead of LDS; the AD / length
+    // blocks and the virtual blocks still come from LDS.  Measured on C1:
+    // seal 12.8 / open 12.6 ms against 10.2 / 9.9 from LDS (the 11-byte
+    // misaligned 16-byte global loads are slower than the LDS queue)
+    const uint8_t* ctg = OPEN ? in : out;
+    const uint32_t pre = adlen + 8u;
+    auto a_load = [&](const uint32_t i) -> u32x4 {
+        if (SG_MAC_GLOBAL_A) {
+            const uint32_t si = 32u * (2u * i + hh) + q;
+            const uint32_t jb = si - g.z;
+            if (si >= g.z && 16u * jb >= pre && 16u * jb + 16u <= pre + n) return ldu16(ctg + (16u * jb - pre));
+        }
+        return ldu16(a_at(i));
+    };
     // operands of step i + 1 are loaded while step i runs
-    u32x4 a = ldu16(a_at(0)), b = ldu16(b_at(0));
+    u32x4 a = a_load(0), b = ldu16(b_at(0));
 #if SG_MACX == 4  // experiment: the products without the LDS operand loads
     for (uint32_t i = 0; i < g.k; ++i) {
         acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(__builtin_bit_cast(i32x4, a ^ i),
@@ -1013,7 +1032,7 @@ __device__ __forceinline__ void mfma_mac(const KParams& p, const uint32_t rec, c
 #else
     for (uint32_t i = 0; i < g.k; ++i) {
         const uint32_t nx = i + 1u < g.k ? i + 1u : i;
-        const u32x4 an = ldu16(a_at(nx)), bn = ldu16(b_at(nx));
+        const u32x4 an = a_load(nx), bn = ldu16(b_at(nx));
         acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(__builtin_bit_cast(i32x4, a ^ 0x80808080u),
                                                      __builtin_bit_cast(i32x4, b), acc, 0, 0, 0);
         a = an;
@@ -1248,6 +1267,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
         }
     }
     if constexpr (!OPEN) {
+        // the MAC reads the stored ciphertext back (SG_MAC_GLOBAL_A): every wave's stores first
+        if (SG_MAC_GLOBAL_A) __syncthreads();
         if (active && w == (rec & 3u) && !SG_LS_NOMAC) mfma_mac<false>(p, rec, n, adlen, slot, S, in, out, lane);
     }
 }
