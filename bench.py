@@ -328,7 +328,7 @@ def main():
     dom_ms = tm[f"{dom}_ms"]
     achieved = alg_bytes / (dom_ms * 1e-3) / 1e9
     traffic, valu = None, None
-    tp = Path(args.traffic or ROOT / "profiles" / ("traffic_r01.json" if args.workload == "c1" else
+    tp = Path(args.traffic or ROOT / "profiles" / ("traffic_r01d.json" if args.workload == "c1" else
                                                    "traffic_r01_c2.json"))
     if tp.exists():
         try:
