@@ -924,15 +924,6 @@ template <bool OPEN>
 __device__ __forceinline__ void mfma_mac(const KParams& p, const uint32_t rec, const uint32_t n, const uint32_t adlen,
                                          uint8_t* slot, const uint32_t S, const uint8_t* in, uint8_t* out,
                                          const uint32_t lane) {
-#ifndef SG_MAC_PRIO
-#define SG_MAC_PRIO 0
-#endif
-#ifndef SG_MACX
-#define SG_MACX 0  // timing experiments only: stop the MAC after stage 1 (power table), 2 (MFMA), 3 (transpose)
-#endif
-    // The MAC wave runs beside other workgroups' lock-step rounds on its SIMD;
-    // at equal priority its latency chain stretches and holds the record's LDS
-    if (SG_MAC_PRIO) __builtin_amdgcn_s_setprio(SG_MAC_PRIO);
     const MacGeom g = mac_geom(adlen, n, 64u);
     const uint32_t rows = 2u * g.k;
     const uint32_t* kr = p.ws + (uint64_t)rec * kKeyRecWordsLs;
@@ -979,7 +970,6 @@ __device__ __forceinline__ void mfma_mac(const KParams& p, const uint32_t rec, c
         st16(F + 32, u32x4{0u, 0u, 0u, 0u});
     }
     wave_lds_sync();
-    if (SG_MACX == 1) return;
     // ---- S = A B on the matrix cores: lane = (half h, row/column q) ----------
     const uint32_t q = lane & 31u, hh = lane >> 5;
     const uint32_t zoff = S + adlen + 8u + n + 8u;  // 16 zero bytes behind le64(n): the virtual blocks
@@ -988,13 +978,9 @@ __device__ __forceinline__ void mfma_mac(const KParams& p, const uint32_t rec, c
     for (int i = 0; i < 16; ++i) acc[i] = 1 << 24;
     auto a_at = [&](const uint32_t i) {
         const uint32_t si = 32u * (2u * i + hh) + q;  // lanes q read consecutive blocks
-        const uint32_t o = si < g.z ? zoff : S + 16u * (si - g.z);
-        return slot + ((SG_MACX == 6 || SG_MACX == 8) ? (o & ~15u) : o);  // 6, 8: timing experiments, aligned A
+        return slot + (si < g.z ? zoff : S + 16u * (si - g.z));
     };
-    auto b_at = [&](const uint32_t i) {
-        const uint32_t o = 48u * (2u * i + hh) + 31u - q;
-        return slot + ((SG_MACX == 7 || SG_MACX == 8) ? (o & ~15u) : o);  // 7, 8: timing experiments, aligned B
-    };
+    auto b_at = [&](const uint32_t i) { return slot + 48u * (2u * i + hh) + 31u - q; };
 #ifndef SG_MAC_GLOBAL_A
 #define SG_MAC_GLOBAL_A 0
 #endif
@@ -1016,20 +1002,6 @@ __device__ __forceinline__ void mfma_mac(const KParams& p, const uint32_t rec, c
     };
     // operands of step i + 1 are loaded while step i runs
     u32x4 a = a_load(0), b = ldu16(b_at(0));
-#if SG_MACX == 4  // experiment: the products without the LDS operand loads
-    for (uint32_t i = 0; i < g.k; ++i) {
-        acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(__builtin_bit_cast(i32x4, a ^ i),
-                                                     __builtin_bit_cast(i32x4, b), acc, 0, 0, 0);
-    }
-#elif SG_MACX == 5  // experiment: the LDS operand loads without the products
-    for (uint32_t i = 0; i < g.k; ++i) {
-        const uint32_t nx = i + 1u < g.k ? i + 1u : i;
-        const u32x4 an = ldu16(a_at(nx)), bn = ldu16(b_at(nx));
-        acc[i & 15] += (int)(a.x ^ b.y ^ a.w ^ b.z);
-        a = an;
-        b = bn;
-    }
-#else
     for (uint32_t i = 0; i < g.k; ++i) {
         const uint32_t nx = i + 1u < g.k ? i + 1u : i;
         const u32x4 an = a_load(nx), bn = ldu16(b_at(nx));
@@ -1038,13 +1010,8 @@ __device__ __forceinline__ void mfma_mac(const KParams& p, const uint32_t rec, c
         a = an;
         b = bn;
     }
-#endif
     // ---- transpose through LDS (over the power table), 16 rows at a time:
     // accumulator i of lane (h, q) is S[(i & 3) + 8 (i >> 2) + 4 h][q]; lane q' < 32 takes row q'
-    if (SG_MACX == 2 || SG_MACX == 4 || SG_MACX == 5) {
-        if (lane == 0 && acc[0] == 12345 && acc[15] == 54321) p.status[rec] = 7;  // keep the product live
-        return;
-    }
     uint32_t X[32];
     wave_lds_sync();
 #pragma unroll
@@ -1065,10 +1032,6 @@ __device__ __forceinline__ void mfma_mac(const KParams& p, const uint32_t rec, c
             }
         }
         wave_lds_sync();
-    }
-    if (SG_MACX == 3) {
-        if (lane == 0 && X[0] == 12345 && X[31] == 54321) p.status[rec] = 7;
-        return;
     }
     // ---- X_q = sum_c S'[q][c] 2^(8c) (radix 2^32, 9 words): the four byte
     // phases c = 4m + j are each a run of non-overlapping 25-bit words
