@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=4096, help="records in the CPU-baseline sample")
     ap.add_argument("--cpu-seconds", type=float, default=2.0, help="min wall time of the CPU baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-bitexact", action="store_true",
+                    help="skip the oracle tag fold / sample compare of the last step (C1)")
     ap.add_argument("--sg-records", type=int, default=16384,
                     help="records per rank moved by the separately timed RCCL scatter/gather (N > 1; 0 = off)")
     ap.add_argument("--strong", action="store_true",
@@ -70,7 +72,7 @@ def cpu_baseline(args, n):
 
     o = get_oracle()
     count = args.cpu_sample
-    threads = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()))
+    threads = host_threads()
     pt = np.empty(count * n, dtype=np.uint8)
     ct = np.empty(count * (n + 16), dtype=np.uint8)
     back = np.empty(count * n, dtype=np.uint8)
@@ -129,8 +131,46 @@ def cpu_baseline(args, n):
         "sample": f"{count} x {n} B TLS records seal+open, x{reps} repetitions, {threads} threads "
                   f"(oracle/suruga_oracle.c, the reference's scalar algorithm)",
         "single_thread_gibs": round(one, 4), "cpu": model or platform.processor(),
+        "host_logical_cpus": os.cpu_count(),
+        "cores_note": "threads = every CPU in this process's affinity mask (os.sched_getaffinity); "
+                      "host_logical_cpus = all logical CPUs of the machine",
         "optimised_cpu": ossl,
     }
+
+
+def host_threads() -> int:
+    """Every CPU this process may run on (the box's CPU share), uncapped."""
+    if hasattr(os, "sched_getaffinity"):
+        return max(1, len(os.sched_getaffinity(0)))
+    return max(1, os.cpu_count() or 1)
+
+
+def bitexact_check(ct, n, count, seq0):
+    """Outside the timed region: the XOR-fold of every one of the batch's tags
+    against the oracle's multithreaded fold of the same records (fill rule,
+    seq = seq0 + i, chacha20_poly1305.rs:48-59), plus a byte-for-byte compare of
+    a strided sample of whole records (ct || tag).  Test infrastructure only:
+    the oracle checks, it is never the measured path."""
+    import numpy as np
+
+    sys.path.insert(0, str(ROOT / "tests"))
+    from oracle_ffi import oracle as get_oracle  # checker only
+
+    o = get_oracle()
+    rows = ct.view(count, n + 16)
+    tags = rows[:, n:].cpu().numpy()
+    fold = np.bitwise_xor.reduce(tags, axis=0).tobytes()
+    t0 = time.perf_counter()
+    ref_fold = o.tag_fold_tls(KEY, seq0, SEED, seq0, n, count, host_threads())
+    fold_s = time.perf_counter() - t0
+    idx = sorted(set([0, 1, count // 2, count - 1] + list(range(0, count, 4099))))
+    sample_ok = True
+    for i in idx:
+        pt = o.fill_record(SEED, seq0 + i, n)
+        exp = o.seal(KEY, (seq0 + i).to_bytes(8, "big"), pt, o.tls_ad(seq0 + i, n))
+        sample_ok = sample_ok and rows[i].cpu().numpy().tobytes() == exp
+    return {"bitexact_fold": fold == ref_fold, "fold_records": count, "bitexact_sample": sample_ok,
+            "sample_records": len(idx), "oracle_fold_s": round(fold_s, 2)}
 
 
 def measure_scatter_gather(args, dist, backend, rank, world, dev, n, count, seq0, seal_b, lib, keys, ws, stream):
@@ -227,8 +267,11 @@ def main():
     from suruga_amd import batch as B
     from suruga_amd import shard
 
-    if not _build.LIB.exists():
-        _build.build_library()
+    if not _build.LIB.exists():  # normally prebuilt in-tree; only rank 0 builds, the others wait
+        if rank == 0:
+            _build.build_library()
+        if dist is not None:
+            dist.barrier()
     n = args.record_bytes
     if args.strong:  # total work fixed: rank r owns a contiguous slice of --records
         lo, hi = shard.record_range(args.records, rank, world)
@@ -293,11 +336,17 @@ def main():
     elapsed = shard.timed(dist, step, args.steps, sync=torch.cuda.synchronize,
                           device=dev if backend == "nccl" else None)
 
-    # correctness of the last step (outside the timed region)
+    # correctness of the last step (outside the timed region): every record
+    # round-trips, and (C1) every tag and a sample of records equal the oracle's
     mism = torch.zeros(1, dtype=torch.int64, device=dev)
     B.compare_records(*cmp_args, mism, stream=stream)
     bad_status = int((status != 0).sum().item())
     roundtrip_ok = int(mism.item()) == 0 and bad_status == 0
+    exact = None
+    if args.workload == "c1" and not args.no_bitexact:
+        torch.cuda.synchronize()
+        exact = bitexact_check(ct, n, count, seq0)
+        roundtrip_ok = roundtrip_ok and exact["bitexact_fold"] and exact["bitexact_sample"]
 
     # per-kernel device time with HIP events on the launch stream
     B.set_timing(True)
@@ -327,15 +376,17 @@ def main():
     alg_bytes = alg[dom]
     dom_ms = tm[f"{dom}_ms"]
     achieved = alg_bytes / (dom_ms * 1e-3) / 1e9
-    traffic, valu = None, None
-    tp = Path(args.traffic or ROOT / "profiles" / ("traffic_r01d.json" if args.workload == "c1" else
-                                                   "traffic_r01_c2.json"))
+    traffic, valu, traffic_src = None, None, None
+    tp = Path(args.traffic or ROOT / "profiles" / ("traffic_r02.json" if args.workload == "c1" else
+                                                   "traffic_r02_c2.json"))
     if tp.exists():
         try:
             tj = json.loads(tp.read_text())
             if tj.get("records") == count and tj.get("record_bytes") == cfg["record_bytes"] and \
                     tj.get("kernels", lib.sg_build_info().decode()) == lib.sg_build_info().decode():
                 traffic = tj.get(f"{dom}_bytes_per_launch")
+                traffic_src = (f"profiles/{tp.name}: rocprofv3 PMC FETCH_SIZE x 2 + WRITE_SIZE of this kernel build "
+                               "in a separate profiling run (not this run)") if traffic else None
                 vpr = tj.get(f"{dom}_valu_per_record")
                 if vpr:
                     # VALU issue account of the same kernel: PMC SQ_INSTS_VALU per record (a
@@ -349,6 +400,11 @@ def main():
         except (ValueError, OSError):
             traffic = None
 
+    wpr_on = args.workload == "c1" and n == 16384 and lib.sg_set_lockstep(-1) == 1
+    if args.workload == "c1":
+        dom_kernel = f"sg_wpr_kernel<{dom.upper()}>" if wpr_on else f"sg_aead_kernel<{dom.upper()}, 256>"
+    else:
+        dom_kernel = f"sg_classify_kernel + sg_aead_list_kernel<{dom.upper()}, L=2..256> (one batch)"
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline and args.workload == "c1":
@@ -359,11 +415,9 @@ def main():
             "higher_is_better": True, "scaling": "strong" if args.strong else "weak", "vs_baseline": None, "dtype": "u32",
             "data": "synthetic (splitmix64 records generated on device)",
             "config": dict(cfg, parallelism=f"record-shard x{world}", kernels=lib.sg_build_info().decode()),
-            "roofline": {"bound": "hbm", "kernel": (f"sg_aead_kernel<{dom.upper()}, 256>" if args.workload == "c1" else
-                                                    f"sg_classify_kernel + sg_aead_list_kernel<{dom.upper()}, L=2..256> "
-                                                    "(one batch)"),
+            "roofline": {"bound": "hbm", "kernel": dom_kernel,
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
                          "alg_bytes_per_launch": alg_bytes, "avg_launch_ms": round(dom_ms, 4)},
             "valu_roofline": valu,
             "kernel_ms": {"seal": round(tm["seal_ms"], 4), "open": round(tm["open_ms"], 4),
@@ -372,6 +426,8 @@ def main():
             "correct": roundtrip_ok,
             "cpu_baseline": cpu,
         }
+        if exact is not None:
+            line.update(exact)
         if scatter_gather is not None:
             line["scatter_gather"] = scatter_gather
         print(json.dumps(line), flush=True)

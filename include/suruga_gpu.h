@@ -126,7 +126,9 @@ typedef struct sg_batch {
      *   open: input = ct || tag of len_i bytes (len_i >= 16 else status
      *         SG_E_SHORT), output = plaintext (len_i - 16)
      * len_i = len ? len[i] : uniform_len.  max_len >= every len_i is required
-     * when len != NULL (it sizes the LDS staging of one record).              */
+     * when len != NULL (it sizes the LDS staging of one record); a longer
+     * record is skipped and the call returns SG_E_ARG (under stream capture it
+     * is skipped silently).                                                    */
     const uint8_t*  in;
     const uint64_t* in_off;
     uint64_t        in_stride;
@@ -137,22 +139,33 @@ typedef struct sg_batch {
     uint32_t        uniform_len;
     uint32_t        max_len;
 
-    /* open: per-record status (SG_OK / SG_E_BAD_MAC / SG_E_SHORT), device   */
+    /* open: per-record status, device: SG_OK / SG_E_BAD_MAC / SG_E_SHORT, or
+     * SG_STATUS_SKIPPED for a record longer than max_len (not processed)    */
     uint8_t*        status;
 
-    /* HIP stream (hipStream_t) or NULL for the library's per-device stream.
-     * The call is asynchronous on that stream when `stream` is non-NULL,
-     * except that a mixed-size batch (len != NULL, records in more than one
-     * size class) waits once for its classification so that every class runs
-     * on an exact grid.  Under stream capture it does not wait (persistent
-     * class grids), so the whole call is graph-capturable with a workspace. */
+    /* HIP stream (hipStream_t).  Non-NULL: the call is asynchronous on that
+     * stream, except that a mixed-size batch (len != NULL, records in more
+     * than one size class) waits once for its classification so that every
+     * class runs on an exact grid; under stream capture it does not wait
+     * (persistent class grids), so the whole call is graph-capturable with a
+     * caller workspace.  NULL: the null (default) stream -- ordered after the
+     * caller's earlier work on it -- and the call returns when the batch is
+     * done.  No library lock is held while a call waits, so calls on
+     * different streams (e.g. a writer and a reader thread, client.rs:19-24)
+     * run concurrently on the device. */
     void*           stream;
 
-    /* scratch of >= sg_workspace_size(count) bytes of device memory, or NULL
-     * to use a library-owned cache (grown on demand; not graph-capturable). */
+    /* scratch of >= sg_workspace_size(count) bytes of 16-byte aligned device
+     * memory, or NULL to use a library-owned cache: each call takes a buffer
+     * no other call is enqueuing on and orders its reuse on the device with an
+     * event, so asynchronous calls on different streams never share scratch.
+     * A call under stream capture must pass a workspace. */
     void*           workspace;
     size_t          workspace_size;
 } sg_batch;
+
+#define SG_STATUS_SKIPPED 3  /* open status of a record with len_i > max_len;
+                                sg_*_batch then returns SG_E_ARG            */
 
 size_t sg_workspace_size(uint32_t count);
 
@@ -266,12 +279,14 @@ int sg_set_timing(int enable);
 int sg_timing_read(double* seal_ms, double* open_ms, double* keying_ms,
                    uint32_t* n_seal, uint32_t* n_open, uint32_t* n_keying);
 
-/* Kernel form for uniform batches of 8 KiB < n <= 16 KiB records (C1):
- * 1 = lock-step kernel (two records per 512-thread workgroup, MAC on all 256
- * lanes), 0 = the size-class kernel used for every other batch.  Both are
- * bit-exact; the switch exists for A/B measurement and for tests that cover
- * both.  Initial value: environment SG_LOCKSTEP ("0"/"1"), else the build
- * default.  Returns the previous setting; a negative argument only queries. */
+/* Kernel form for uniform batches of full 16 KiB records (n = 2^14, the
+ * size TlsWriter::write_data gives every record but a stream's tail; C1):
+ * 1 = the wave-per-record kernel (one wave per record, lock-step ChaCha20
+ * rounds, Poly1305 on the matrix cores fed from the ciphertext registers),
+ * 0 = the size-class kernel used for every other batch.  Both are bit-exact;
+ * the switch exists for A/B measurement and for tests that cover both.
+ * Initial value: environment SG_LOCKSTEP ("0"/"1"), else 1.  Returns the
+ * previous setting; a negative argument only queries. */
 int sg_set_lockstep(int enable);
 
 #ifdef __cplusplus

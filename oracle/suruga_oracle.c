@@ -390,3 +390,57 @@ size_t so_open_batch_tls(const uint8_t key[32], uint64_t seq0, const uint8_t* ct
                          size_t count, uint8_t* pt, uint8_t* status, int threads) {
     return so_run(key, seq0, ct, n, count, pt, status, threads, 1);
 }
+
+/* XOR-fold of the tags of `count` TLS records sealed with seq = seq0 + i and
+ * plaintext record j0 + i of the fill rule (so_fill_record), computed without
+ * materialising the batch: the checker of a full-size device run (bench.py
+ * folds the device's tags the same way).  Test infrastructure only. */
+typedef struct {
+    const uint8_t* key;
+    uint64_t seq0, seed, j0;
+    size_t n, begin, end;
+    uint8_t fold[16];
+} so_fold_job;
+
+static void* so_fold_worker(void* arg) {
+    so_fold_job* j = (so_fold_job*)arg;
+    uint8_t* pt = (uint8_t*)malloc(j->n ? j->n : 1);
+    uint8_t* ct = (uint8_t*)malloc(j->n + 16);
+    uint8_t nonce[8], ad[13];
+    memset(j->fold, 0, 16);
+    for (size_t i = j->begin; i < j->end; ++i) {
+        uint64_t seq = j->seq0 + i;
+        so_fill_record(j->seed, j->j0 + i, pt, j->n);
+        so_u64_be(seq, nonce);
+        so_tls_ad(seq, 23, 3, 3, (uint16_t)j->n, ad);
+        so_seal(j->key, nonce, pt, j->n, ad, 13, ct);
+        for (int b = 0; b < 16; ++b) j->fold[b] ^= ct[j->n + b];
+    }
+    free(pt);
+    free(ct);
+    return NULL;
+}
+
+void so_tag_fold_tls(const uint8_t key[32], uint64_t seq0, uint64_t seed, uint64_t j0, size_t n, size_t count,
+                     int threads, uint8_t out[16]) {
+    if (threads < 1) threads = 1;
+    if (count > 0 && (size_t)threads > count) threads = (int)count;
+    so_fold_job* jobs = (so_fold_job*)calloc((size_t)threads, sizeof(so_fold_job));
+    pthread_t* tids = (pthread_t*)calloc((size_t)threads, sizeof(pthread_t));
+    size_t per = (count + (size_t)threads - 1) / (size_t)threads;
+    for (int t = 0; t < threads; ++t) {
+        so_fold_job* j = &jobs[t];
+        j->key = key; j->seq0 = seq0; j->seed = seed; j->j0 = j0; j->n = n;
+        j->begin = (size_t)t * per < count ? (size_t)t * per : count;
+        j->end = j->begin + per < count ? j->begin + per : count;
+        if (threads == 1) so_fold_worker(j);
+        else pthread_create(&tids[t], NULL, so_fold_worker, j);
+    }
+    memset(out, 0, 16);
+    for (int t = 0; t < threads; ++t) {
+        if (threads > 1) pthread_join(tids[t], NULL);
+        for (int b = 0; b < 16; ++b) out[b] ^= jobs[t].fold[b];
+    }
+    free(jobs);
+    free(tids);
+}

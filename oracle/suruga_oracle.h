@@ -96,4 +96,9 @@ size_t so_open_batch_tls(const uint8_t key[32], uint64_t seq0, const uint8_t* ct
 #ifdef __cplusplus
 }
 #endif
+/* XOR-fold of the tags of count TLS records (seq = seq0 + i, plaintext =
+ * fill-rule record j0 + i) without materialising them. */
+void so_tag_fold_tls(const uint8_t key[32], uint64_t seq0, uint64_t seed, uint64_t j0, size_t n, size_t count,
+                     int threads, uint8_t out[16]);
+
 #endif

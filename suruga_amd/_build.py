@@ -23,8 +23,10 @@ LIB = PKG / "libsuruga_gpu.so"
 ORACLE_DIR = ROOT / "oracle"
 ORACLE_LIB = ORACLE_DIR / "liboracle.so"
 
-HIP_SOURCES = [CSRC / "sg_kernels.hip", CSRC / "sg_capi.cpp", CSRC / "sg_record.cpp", CSRC / "sg_keysched.cpp"]
-HIP_DEPS = HIP_SOURCES + [CSRC / "sg_internal.h", CSRC / "sg_host.h", CSRC / "sg_chacha_grp.inc", ROOT / "include" / "suruga_gpu.h"]
+HIP_SOURCES = [CSRC / "sg_kernels.hip", CSRC / "sg_wpr.hip", CSRC / "sg_capi.cpp", CSRC / "sg_record.cpp",
+               CSRC / "sg_keysched.cpp"]
+HIP_DEPS = HIP_SOURCES + [CSRC / "sg_internal.h", CSRC / "sg_device.h", CSRC / "sg_host.h", CSRC / "sg_chacha_grp.inc",
+                          ROOT / "include" / "suruga_gpu.h"]
 ORACLE_SOURCES = [ORACLE_DIR / "suruga_oracle.c"]
 ORACLE_DEPS = ORACLE_SOURCES + [ORACLE_DIR / "suruga_oracle.h"]
 
@@ -48,12 +50,24 @@ def hipcc() -> str:
     return str(cand) if cand.exists() else "hipcc"
 
 
+# Switches of earlier timing experiments that produced wrong tags.  They are
+# gone from the product sources (tests/test_abi.py checks), and a build of the
+# product library refuses them outright.
+FORBIDDEN_DEFINE_PREFIXES = ("-DSG_LS_NO", "-DSG_LS_COMPILED", "-DSG_EXP_", "-DSG_MAC_GLOBAL_A", "-DSG_MACX")
+
+
 def build_library(force: bool = False, out: Path | None = None, defines=()) -> Path:
     """Compile the gfx950 HIP library (seconds).  ``out``/``defines`` build an
-    experiment variant (e.g. ``-DSG_SALU_PRE=0``) next to the product library."""
+    experiment variant (e.g. ``-DSG_SALU_PRE=0``) next to the product library;
+    the product library itself is only ever built without defines."""
     target = Path(out) if out else LIB
+    bad = [d for d in defines if str(d).startswith(FORBIDDEN_DEFINE_PREFIXES)]
+    if bad:
+        raise ValueError(f"wrong-output experiment switches are not buildable: {bad}")
+    if defines and target.resolve() == LIB.resolve():
+        raise ValueError("the product library is built without -D switches; pass out= for a variant")
     if force or defines or _stale(target, HIP_DEPS):
-        tmp = target.with_suffix(".so.tmp")
+        tmp = target.with_suffix(f".so.tmp{os.getpid()}")  # concurrent builders never share a temp file
         _run([hipcc(), "--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17",
               "-Wall", "-Wno-unused-result", *defines, "-o", str(tmp), *map(str, HIP_SOURCES)])
         os.replace(tmp, target)
@@ -63,7 +77,7 @@ def build_library(force: bool = False, out: Path | None = None, defines=()) -> P
 def build_oracle(force: bool = False) -> Path:
     """Compile the CPU restatement used as the parity checker."""
     if force or _stale(ORACLE_LIB, ORACLE_DEPS):
-        tmp = ORACLE_LIB.with_suffix(".so.tmp")
+        tmp = ORACLE_LIB.with_suffix(f".so.tmp{os.getpid()}")
         _run(["gcc", "-O2", "-std=c11", "-Wall", "-Wextra", "-fPIC", "-shared", "-pthread",
               "-o", str(tmp), *map(str, ORACLE_SOURCES)])
         os.replace(tmp, ORACLE_LIB)
@@ -82,7 +96,7 @@ def build_cpp_tests(force: bool = False) -> Path:
     both in-tree libraries."""
     lib, orc = build_library(), build_oracle()
     if force or _stale(CPP_TEST_BIN, CPP_TEST_DEPS + [lib, orc]):
-        tmp = CPP_TEST_BIN.with_suffix(".tmp")
+        tmp = CPP_TEST_BIN.with_suffix(f".tmp{os.getpid()}")
         _run(["g++", "-std=c++17", "-O1", "-Wall", "-Wextra", "-o", str(tmp), str(CPP_TEST_SRC),
               f"-L{lib.parent}", f"-L{orc.parent}", "-lsuruga_gpu", "-loracle",
               "-Wl,-rpath,$ORIGIN/../../suruga_amd:$ORIGIN/../../oracle"])
@@ -100,7 +114,7 @@ def build_ossl(force: bool = False):
     if not Path("/usr/include/openssl/evp.h").exists():
         return OSSL_LIB if OSSL_LIB.exists() else None
     if force or _stale(OSSL_LIB, [OSSL_SRC]):
-        tmp = OSSL_LIB.with_suffix(".so.tmp")
+        tmp = OSSL_LIB.with_suffix(f".so.tmp{os.getpid()}")
         _run(["gcc", "-O2", "-std=c11", "-Wall", "-fPIC", "-shared", "-pthread", "-o", str(tmp), str(OSSL_SRC),
               "-lcrypto"])
         os.replace(tmp, OSSL_LIB)

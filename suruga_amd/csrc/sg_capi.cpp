@@ -48,15 +48,26 @@ using sg::hip_fail;
 #define SG_SINGLE_ZEROCOPY 1
 #endif
 
+// A workspace of the library-owned cache.  Calls with no caller workspace
+// take one that no other call is enqueuing on, make their stream wait for its
+// previous user's work (`done`) and record `done` again after their launches,
+// so reuse is ordered on the device even across streams and asynchronous
+// calls; the host never blocks on it except to grow a buffer.
+struct CachedWs {
+    void* ptr = nullptr;
+    size_t bytes = 0;
+    hipEvent_t done = nullptr;
+    bool used = false;   // `done` has been recorded
+    bool held = false;   // a call is enqueuing on it
+};
+
 struct DeviceState {
     bool init = false;
     bool ok = false;
-    hipStream_t stream = nullptr;
-    void* ws = nullptr;
-    size_t ws_bytes = 0;
+    std::vector<CachedWs*> pool;  // guarded by g_mu
 };
 
-std::mutex g_mu;
+std::mutex g_mu;  // device table, workspace pool bookkeeping (never held across a launch or a wait)
 std::vector<DeviceState> g_dev;
 
 // timing
@@ -64,11 +75,12 @@ struct TimedLaunch {
     hipEvent_t a, b;
     int kind;  // 0 keying, 1 seal, 2 open
 };
+std::mutex g_timing_mu;
 bool g_timing = false;
 std::vector<TimedLaunch> g_timed;
 std::vector<hipEvent_t> g_event_pool;
 
-hipEvent_t get_event() {
+hipEvent_t get_event() {  // caller holds g_timing_mu
     if (!g_event_pool.empty()) {
         hipEvent_t e = g_event_pool.back();
         g_event_pool.pop_back();
@@ -79,7 +91,7 @@ hipEvent_t get_event() {
     return e;
 }
 
-// Checks the device is a gfx950 part and creates its stream.  Caller holds g_mu.
+// Checks the device is a gfx950 part.  Caller holds g_mu.
 int device_state(int dev, DeviceState** out) {
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
@@ -95,8 +107,6 @@ int device_state(int dev, DeviceState** out) {
             d.ok = false;
             return fail(SG_E_NODEV, "device is %s, this library is built for gfx950 only", prop.gcnArchName);
         }
-        SG_HIP(hipSetDevice(dev));
-        SG_HIP(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
         d.ok = true;
     }
     if (!d.ok) return fail(SG_E_NODEV, "device not usable%s");
@@ -104,26 +114,48 @@ int device_state(int dev, DeviceState** out) {
     return SG_OK;
 }
 
-int current_device_state(DeviceState** out) {
-    int dev = 0;
-    SG_HIP(hipGetDevice(&dev));
-    return device_state(dev, out);
+// Take a cached workspace of >= need bytes for a call on stream s (the current
+// device is d's).  Growing a buffer waits for its previous user only.
+int ws_acquire(DeviceState* d, size_t need, hipStream_t s, CachedWs** out) {
+    CachedWs* w = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        for (CachedWs* c : d->pool)
+            if (!c->held && (!w || (c->bytes >= need && (w->bytes < need || c->bytes < w->bytes)))) w = c;
+        if (!w) {
+            w = new CachedWs();
+            d->pool.push_back(w);
+        }
+        w->held = true;
+    }
+    auto release_on_error = [&](int rc) {
+        std::lock_guard<std::mutex> lk(g_mu);
+        w->held = false;
+        return rc;
+    };
+    if (!w->done && hipEventCreateWithFlags(&w->done, hipEventDisableTiming) != hipSuccess)
+        return release_on_error(fail(SG_E_HIP, "hipEventCreate failed%s"));
+    if (w->bytes < need) {
+        if (w->used && hipEventSynchronize(w->done) != hipSuccess)
+            return release_on_error(fail(SG_E_HIP, "workspace event wait failed%s"));
+        if (w->ptr) (void)hipFree(w->ptr);
+        w->ptr = nullptr;
+        w->bytes = 0;
+        const size_t sz = need < (1u << 20) ? (1u << 20) : need;
+        if (hipMalloc(&w->ptr, sz) != hipSuccess) return release_on_error(fail(SG_E_HIP, "workspace hipMalloc failed%s"));
+        w->bytes = sz;
+        w->used = false;
+    }
+    if (w->used && hipStreamWaitEvent(s, w->done, 0) != hipSuccess)
+        return release_on_error(fail(SG_E_HIP, "hipStreamWaitEvent failed%s"));
+    *out = w;
+    return SG_OK;
 }
 
-// Workspace from the per-device cache.  Caller holds g_mu.  Growing it frees
-// the old buffer, so it synchronises the device first.
-int cached_workspace(DeviceState* d, size_t need, void** ws) {
-    if (d->ws_bytes < need) {
-        SG_HIP(hipDeviceSynchronize());
-        if (d->ws) SG_HIP(hipFree(d->ws));
-        d->ws = nullptr;
-        d->ws_bytes = 0;
-        size_t sz = need < (1u << 20) ? (1u << 20) : need;
-        SG_HIP(hipMalloc(&d->ws, sz));
-        d->ws_bytes = sz;
-    }
-    *ws = d->ws;
-    return SG_OK;
+void ws_release(CachedWs* w, hipStream_t s, bool launched) {
+    if (launched && hipEventRecord(w->done, s) == hipSuccess) w->used = true;
+    std::lock_guard<std::mutex> lk(g_mu);
+    w->held = false;
 }
 
 int validate(const sg_batch* b, bool open) {
@@ -148,25 +180,20 @@ int validate(const sg_batch* b, bool open) {
     return SG_OK;
 }
 
-int run_batch(const sg_batch* b, bool open) {
-    int rc = validate(b, open);
-    if (rc != SG_OK || b->count == 0) return rc;
+// The wave-per-record kernel (sg_wpr.hip) takes uniform batches of full
+// 16 KiB records in a 16-byte aligned strided layout; everything else runs on
+// the size-class kernels.
+bool wpr_eligible(const sg_batch* b, bool open) {
+    if (!sg::wpr_enabled() || b->len || b->in_off || b->out_off) return false;
+    if (b->uniform_len != (open ? sg::kWprN + SG_MAC_LEN : sg::kWprN)) return false;
+    // per-record scalars are read as dwords: key index, sequence numbers, nonces
+    if (((uintptr_t)b->key_index | (uintptr_t)b->seq) % 4u) return false;
+    if (!(b->flags & SG_BATCH_TLS) && (uintptr_t)b->nonces % 4u) return false;
+    return ((uintptr_t)b->in | (uintptr_t)b->out | b->in_stride | b->out_stride) % 16u == 0u;
+}
 
-    std::lock_guard<std::mutex> lk(g_mu);
-    DeviceState* d = nullptr;
-    rc = current_device_state(&d);
-    if (rc != SG_OK) return rc;
-    hipStream_t s = b->stream ? (hipStream_t)b->stream : d->stream;
-
-    void* ws = b->workspace;
-    const size_t need = sg_workspace_size(b->count);
-    if (ws) {
-        if (b->workspace_size < need) return fail(SG_E_ARG, "workspace too small%s");
-    } else {
-        rc = cached_workspace(d, need, &ws);
-        if (rc != SG_OK) return rc;
-    }
-
+// Keying + AEAD launches of one batch on stream s with workspace ws.
+int launch_batch(const sg_batch* b, bool open, hipStream_t s, void* ws) {
     sg::KParams p;
     std::memset(&p, 0, sizeof p);
     p.keys = b->keys;
@@ -193,25 +220,73 @@ int run_batch(const sg_batch* b, bool open) {
     const uint32_t maxl = b->len ? b->max_len : b->uniform_len;
     const uint32_t max_n = open ? (maxl >= 16u ? maxl - 16u : 0u) : maxl;
     const bool uniform = !b->len || sg::size_class(max_n) == 0u;
-    p.ls = (!b->len && sg::lockstep_enabled() && sg::ls_eligible(max_n, p.ad_len)) ? 1u : 0u;
+    const bool wpr = wpr_eligible(b, open);
     uint32_t* lists = p.ws + (size_t)b->count * sg::kKeyRecWordsMax;
     uint32_t* counts = lists + (uint64_t)sg::kNumClasses * b->count;
 
     hipEvent_t e[4] = {nullptr, nullptr, nullptr, nullptr};
-    if (g_timing)
-        for (auto& x : e) x = get_event();
-    if (g_timing) SG_HIP(hipEventRecord(e[0], s));
-    SG_HIP(sg::launch_keying(p, open, s));
-    if (g_timing) {
-        SG_HIP(hipEventRecord(e[1], s));
-        SG_HIP(hipEventRecord(e[2], s));
+    bool timing = false;
+    {
+        std::lock_guard<std::mutex> lk(g_timing_mu);
+        timing = g_timing;
+        if (timing)
+            for (auto& x : e) x = get_event();
     }
-    SG_HIP(sg::launch_aead(p, open, max_n, uniform, lists, counts, s));
-    if (g_timing) {
+    if (timing) SG_HIP(hipEventRecord(e[0], s));
+    if (wpr) {
+        SG_HIP(sg::launch_wpr(p, open, s, timing ? e[1] : nullptr, timing ? e[2] : nullptr));
+    } else {
+        SG_HIP(sg::launch_keying(p, open, s));
+        if (timing) {
+            SG_HIP(hipEventRecord(e[1], s));
+            SG_HIP(hipEventRecord(e[2], s));
+        }
+        uint32_t over = 0;
+        SG_HIP(sg::launch_aead(p, open, max_n, uniform, lists, counts, s, &over));
+        if (over) return fail(SG_E_ARG, "records longer than max_len were not processed%s");
+    }
+    if (timing) {
         SG_HIP(hipEventRecord(e[3], s));
+        std::lock_guard<std::mutex> lk(g_timing_mu);
         g_timed.push_back({e[0], e[1], 0});
         g_timed.push_back({e[2], e[3], open ? 2 : 1});
     }
+    return SG_OK;
+}
+
+int run_batch(const sg_batch* b, bool open) {
+    int rc = validate(b, open);
+    if (rc != SG_OK || b->count == 0) return rc;
+
+    int dev = 0;
+    SG_HIP(hipGetDevice(&dev));
+    DeviceState* d = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        rc = device_state(dev, &d);
+    }
+    if (rc != SG_OK) return rc;
+    // NULL = the null stream: ordered after the caller's earlier work on it
+    // (torch's default stream is the null stream), and the call is synchronous
+    hipStream_t s = (hipStream_t)b->stream;
+
+    void* ws = b->workspace;
+    CachedWs* cws = nullptr;
+    const size_t need = sg_workspace_size(b->count);
+    if (ws) {
+        if (b->workspace_size < need) return fail(SG_E_ARG, "workspace too small%s");
+        if ((uintptr_t)ws % 16u) return fail(SG_E_ARG, "workspace must be 16-byte aligned%s");
+    } else {
+        hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+        SG_HIP(hipStreamIsCapturing(s, &cap));
+        if (cap != hipStreamCaptureStatusNone)
+            return fail(SG_E_ARG, "a call under stream capture needs a caller workspace%s");
+        if ((rc = ws_acquire(d, need, s, &cws)) != SG_OK) return rc;
+        ws = cws->ptr;
+    }
+    rc = launch_batch(b, open, s, ws);
+    if (cws) ws_release(cws, s, true);
+    if (rc != SG_OK) return rc;
     if (!b->stream) SG_HIP(hipStreamSynchronize(s));
     return SG_OK;
 }
@@ -231,10 +306,16 @@ size_t sg_fixed_iv_len(void) { return 0; }
 size_t sg_mac_len(void) { return SG_MAC_LEN; }
 int sg_abi_version(void) { return SG_ABI_VERSION; }
 const char* sg_last_error(void) { return g_err.c_str(); }
-const char* sg_build_info(void) { return sg::kernel_config(); }
+const char* sg_build_info(void) {
+    static const std::string on = std::string("gfx950 ") + sg::wpr_kernel_config() + "; other batches: " +
+                                  sg::class_kernel_config();
+    static const std::string off = std::string("gfx950 ") + sg::class_kernel_config() + " (wave-per-record kernel off)";
+    return sg::wpr_enabled() ? on.c_str() : off.c_str();
+}
 size_t sg_workspace_size(uint32_t count) {
-    // keying records, one list per size class, one list counter per class
-    return (size_t)count * (sg::kKeyRecWordsMax + sg::kNumClasses) * 4u + sg::kNumClasses * 4u;
+    // keying records, one list per size class, the class populations and the
+    // count of records longer than max_len
+    return (size_t)count * (sg::kKeyRecWordsMax + sg::kNumClasses) * 4u + (sg::kNumClasses + 1u) * 4u;
 }
 
 sg_ctx* sg_ctx_new(const uint8_t key[32], int device) {
@@ -247,7 +328,8 @@ sg_ctx* sg_ctx_new(const uint8_t key[32], int device) {
         DeviceState* d = nullptr;
         if (device_state(device, &d) != SG_OK) return nullptr;
     }
-    if (hipSetDevice(device) != hipSuccess) {
+    sg::DeviceGuard dg(device);
+    if (!dg.ok) {
         fail(SG_E_HIP, "hipSetDevice failed%s");
         return nullptr;
     }
@@ -273,7 +355,7 @@ sg_ctx* sg_ctx_new(const uint8_t key[32], int device) {
 
 void sg_ctx_free(sg_ctx* c) {
     if (!c) return;
-    (void)hipSetDevice(c->device);
+    sg::DeviceGuard dg(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     sg::record_staging_free(c->rec);
     (void)hipFree(c->d_key);
@@ -298,7 +380,8 @@ static int single(sg_ctx* c, bool open, const uint8_t* nonce, size_t nonce_len, 
     if (n > SG_MAX_RECORD_LEN) return fail(SG_E_ARG, "record longer than SG_MAX_RECORD_LEN%s");
 
     std::lock_guard<std::mutex> lk(c->mu);
-    SG_HIP(hipSetDevice(c->device));
+    sg::DeviceGuard dg(c->device);
+    if (!dg.ok) return fail(SG_E_HIP, "hipSetDevice failed%s");
     std::memcpy(c->h_in, nonce, 8);
     if (adlen) std::memcpy(c->h_in + sg::kSingleAdOff, ad, adlen);
     if (in_len) std::memcpy(c->h_in + sg::kSingleInOff, in, in_len);
@@ -376,13 +459,10 @@ int sg_compare_records(const uint8_t* a, uint64_t sa, const uint8_t* b, uint64_t
     return SG_OK;
 }
 
-int sg_set_lockstep(int enable) {
-    std::lock_guard<std::mutex> lk(g_mu);  // not while a batch is being launched
-    return sg::set_lockstep(enable);
-}
+int sg_set_lockstep(int enable) { return sg::set_wpr(enable); }
 
 int sg_set_timing(int enable) {
-    std::lock_guard<std::mutex> lk(g_mu);
+    std::lock_guard<std::mutex> lk(g_timing_mu);
     for (auto& t : g_timed) {
         (void)hipEventSynchronize(t.b);
         g_event_pool.push_back(t.a);
@@ -395,7 +475,7 @@ int sg_set_timing(int enable) {
 
 int sg_timing_read(double* seal_ms, double* open_ms, double* keying_ms, uint32_t* n_seal, uint32_t* n_open,
                    uint32_t* n_keying) {
-    std::lock_guard<std::mutex> lk(g_mu);
+    std::lock_guard<std::mutex> lk(g_timing_mu);
     double sum[3] = {0, 0, 0};
     uint32_t cnt[3] = {0, 0, 0};
     for (auto& t : g_timed) {

@@ -17,6 +17,23 @@ int hip_fail(hipError_t e, const char* where);
 struct RecordStaging;                   // sg_record.cpp
 void record_staging_free(RecordStaging* rs);
 
+// Makes `dev` the calling thread's current HIP device for a scope and restores
+// the previous one on exit, so a context call never leaves the caller's thread
+// on another device.
+struct DeviceGuard {
+    int prev = -1;
+    bool ok = false;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        ok = hipSetDevice(dev) == hipSuccess;
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+    DeviceGuard(const DeviceGuard&) = delete;
+    DeviceGuard& operator=(const DeviceGuard&) = delete;
+};
+
 }  // namespace sg
 
 #define SG_HIP(call)                                                \

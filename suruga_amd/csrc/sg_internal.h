@@ -15,22 +15,28 @@ constexpr uint32_t kKeyRecWords = 104;    // per-record keying output (u32 words
 //   lo[8][5] = R^j       j = 0..7
 //   hi[8][5] = R^(8 i)   i = 0..7
 // so that MAC lane t = 8a + b scales its partial sum by R^(63-t) = hi[7-a] lo[7-b];
-// The lock-step kernel (KParams::ls, MFMA Poly1305, k from PL = 64 as above)
-// uses a longer record (kKeyRecWordsLs words), radix 2^26, in place of lo/hi:
-//   pl[8][5] = r^(32 j + 1)  j = 0..7   (at kPowLoOff)
-//   ph[6][5] = r^(256 i)     i = 0..5   (at kPowHiOff; P_t = r^(32 t + 1) = ph[t >> 3] pl[t & 7])
-//   rs[8][5] = r^j           j = 0..7
-//   rm[4][5] = r^(8 i)       i = 0..3   (W_q = r^(31 - q) = rm[e >> 3] rs[e & 7])
-//   ctot[5]  = the record's constant term of the MFMA evaluation (mfma_mac)
 constexpr uint32_t kR32Off = 0;
 constexpr uint32_t kSOff = 4;
 constexpr uint32_t kPowLoOff = 8;
 constexpr uint32_t kPowHiOff = 48;
-constexpr uint32_t kRSmallOff = 88;
-constexpr uint32_t kRMidOff = 128;
-constexpr uint32_t kCtotOff = 148;
-constexpr uint32_t kKeyRecWordsLs = 156;
-constexpr uint32_t kKeyRecWordsMax = kKeyRecWordsLs;
+
+// Keying record of the wave-per-record kernel (sg_wpr.hip), u32 words; F26
+// entries are 5 radix-2^26 limbs.  With delta = 0/1 from the geometry
+// (wpr_geom), R = r^4 and T = r^128:
+//   s[4]                                    second half of keystream block 0
+//   ctot[5]                                 the record's constant term
+//   rd[5][5]  = r^(1 + delta + u)          u = 0..4
+//   tk[8][5]  = T^k                         k = 0..7
+//   lo[8][5]  = R^b                         b = 0..7
+//   hi[2][4][5] = 2^(32 h) R^(8 a)          h = 0..1, a = 0..3
+constexpr uint32_t kWS = 0;
+constexpr uint32_t kWCtot = 4;
+constexpr uint32_t kWRd = 12;
+constexpr uint32_t kWTk = 40;
+constexpr uint32_t kWLo = 80;
+constexpr uint32_t kWHi = 120;
+constexpr uint32_t kWprRecWords = 160;
+constexpr uint32_t kKeyRecWordsMax = kWprRecWords;
 
 // Kernel parameters (passed by value as kernarg).
 struct KParams {
@@ -48,7 +54,7 @@ struct KParams {
     uint64_t out_stride;
     const uint32_t* len;
     uint8_t* status;
-    uint32_t* ws;            // count * kKeyRecWords (kKeyRecWordsLs when ls) keying records
+    uint32_t* ws;            // count * kKeyRecWords (kWprRecWords for sg_wpr.hip) keying records
     uint32_t uniform_len;
     uint32_t count;
     uint32_t ad_len;         // explicit mode
@@ -56,7 +62,6 @@ struct KParams {
     uint32_t tls;            // 1 = SG_BATCH_TLS
     uint32_t tls_hdr;        // content_type | major << 8 | minor << 16
     uint32_t lds_rec_bytes;  // LDS bytes per record slot of the launched size class
-    uint32_t ls;             // 1: uniform class-7 batch run by the lock-step kernel (MFMA Poly1305)
 };
 
 // Size classes of the AEAD kernel: class c (0..7) holds records of
@@ -82,35 +87,29 @@ __host__ __device__ inline uint32_t lds_rec_bytes(uint32_t cls, uint32_t adlen, 
     return 32u * PL + ((adlen + 8u + 15u) & ~15u) + ((max_n + 63u) & ~63u) + 64u;
 }
 
-// Lock-step kernel (sg_aead_ls_kernel): two records of one length n per
-// 512-thread workgroup, one 64-byte ChaCha20 block per lane (n <= 16384), and
-// the MAC on one wave per record as an i8 MFMA product (mfma_mac): the slot
-// grid of the PL = 64 geometry (64 k blocks) as 32 rows (slot 32 s + q in
-// row q) of 2k blocks, 2k <= 42.
-// LDS slot: [0, kLsHead) power table (2k rows x 48 B), later the transposed
-// product tile (16 rows x 132 B) | ad || le64(|ad|) (16-rounded) | ct (64-rounded) |
-// le64(n) + zeros.
-constexpr uint32_t kLsHead = 2176;
-constexpr uint32_t kLsTileStride = 132;
-__host__ __device__ inline bool ls_eligible(uint32_t n, uint32_t adlen) {
-    return n > 8192u && n <= 16384u && (adlen + 16u + n + 15u) / 16u <= 64u * 21u;
-}
-__host__ __device__ inline uint32_t lds_ls_rec_bytes(uint32_t adlen, uint32_t n) {
-    return kLsHead + ((adlen + 8u + 15u) & ~15u) + ((n + 63u) & ~63u) + 64u;
-}
-bool lockstep_enabled();  // sg_set_lockstep / SG_LOCKSTEP environment switch
-int set_lockstep(int enable);
+// Wave-per-record kernel (sg_wpr.hip): uniform batches of full 16 KiB TLS
+// records (n = RECORD_MAX_LEN = 2^14, tls.rs:32, the size TlsWriter::write_data
+// gives every record but a stream's tail), 16-byte aligned strided layout, any
+// AD length.  One wave per record, eight records per 512-thread workgroup.
+constexpr uint32_t kWprN = 16384;
+bool wpr_enabled();  // sg_set_lockstep / SG_LOCKSTEP environment switch
+int set_wpr(int enable);
+// keying pre-pass + record kernel; ev_mid (may be NULL) is recorded between them
+hipError_t launch_wpr(const KParams& p, bool open, hipStream_t s, hipEvent_t ev_keyed, hipEvent_t ev_start);
+const char* wpr_kernel_config();
+const char* class_kernel_config();
 
 hipError_t launch_keying(const KParams& p, bool open, hipStream_t s);
 // Seal/open launch.  uniform: every record is in size_class(max_n) (direct
 // launch); otherwise classify into lists[kNumClasses][count] / counts[kNumClasses] and
-// launch per class.
+// launch per class.  counts has kNumClasses + 1 words: the last counts the
+// records longer than max_n, which are skipped (open: status 3); *over
+// receives that count when the populations are read back (not under capture).
 hipError_t launch_aead(const KParams& p, bool open, uint32_t max_n, bool uniform, uint32_t* lists,
-                       uint32_t* counts, hipStream_t s);
+                       uint32_t* counts, hipStream_t s, uint32_t* over);
 hipError_t launch_fill(uint8_t* buf, uint64_t stride, uint32_t len, uint32_t count, uint64_t seed,
                        uint64_t j0, hipStream_t s);
 hipError_t launch_compare(const uint8_t* a, uint64_t sa, const uint8_t* b, uint64_t sb, uint32_t len,
                           uint32_t count, unsigned long long* mism, hipStream_t s);
-const char* kernel_config();
 
 }  // namespace sg

@@ -111,6 +111,23 @@ int drain(RecordStaging::Slot& s) {
     return SG_OK;
 }
 
+// Leaves both pipeline slots idle on every exit path: a call that returns
+// early (a drain or launch error) must not hand a half-finished slot, framed
+// with its own lengths and sequence numbers, to the next call.
+struct SlotReset {
+    RecordStaging* rs;
+    explicit SlotReset(RecordStaging* r) : rs(r) { reset(); }
+    ~SlotReset() { reset(); }
+    void reset() {
+        for (auto& s : rs->slot) {
+            if (s.busy && s.st) (void)hipStreamSynchronize(s.st);
+            s.busy = false;
+            s.nrec = 0;
+            s.first = 0;
+        }
+    }
+};
+
 inline void put_be16(uint8_t* p, uint32_t v) {
     p[0] = (uint8_t)(v >> 8);
     p[1] = (uint8_t)v;
@@ -149,10 +166,12 @@ int64_t sg_write_records(sg_ctx* c, uint64_t seq0, uint8_t content_type, uint8_t
     if (nrec == 0) return 0;
     if (!wire || wire_cap < sg_wire_bound(len)) return fail(SG_E_ARG, "wire buffer too small%s");
     std::lock_guard<std::mutex> lk(c->mu);
-    SG_HIP(hipSetDevice(c->device));
+    DeviceGuard dg(c->device);
+    if (!dg.ok) return fail(SG_E_HIP, "hipSetDevice failed%s");
     RecordStaging* rs = nullptr;
     int rc = staging(c, &rs);
     if (rc != SG_OK) return rc;
+    SlotReset slot_reset(rs);
     size_t wpos = 0;
 
     // frame a drained slot's records into the wire (tls.rs:126-130)
@@ -280,10 +299,12 @@ int sg_read_records(sg_ctx* c, uint64_t seq0, const uint8_t* wire, size_t wire_l
     }
 
     std::lock_guard<std::mutex> lk(c->mu);
-    SG_HIP(hipSetDevice(c->device));
+    DeviceGuard dg(c->device);
+    if (!dg.ok) return fail(SG_E_HIP, "hipSetDevice failed%s");
     RecordStaging* rs = nullptr;
     int rc = staging(c, &rs);
     if (rc != SG_OK) return rc;
+    SlotReset slot_reset(rs);
 
     const uint64_t nrec = recs.size();
     uint64_t next = 0, good = 0, opos = 0, consumed = 0;

@@ -1,0 +1,600 @@
+// sg_wpr.hip -- gfx950 wave-per-record ChaCha20-Poly1305 for full 16 KiB TLS
+// records (klutzy/suruga src/cipher/chacha20_poly1305.rs:48-94 on records of
+// RECORD_MAX_LEN = 2^14 bytes, tls.rs:32,137-147).
+//
+// One wave owns one record; a 512-thread workgroup holds eight records (two
+// waves per SIMD) and walks record groups persistently.  Per record the wave
+// runs four iterations over 4 KiB chunks:
+//
+//   * the chunk arrives lane-contiguously (16 B per lane, 1 KiB per load
+//     instruction, prefetched one chunk ahead into registers) and is staged in
+//     the wave's LDS slice through an XOR swizzle, so that lane t then reads
+//     its own 64-byte block 64 j + t conflict-free;
+//   * lane t computes keystream block 64 j + t + 1 (chacha20.rs:111-135, block
+//     0 being the Poly1305 key, chacha20_poly1305.rs:50-52) with grouped ARX
+//     rounds and an s_barrier after every rotate group (sg_chacha_grp.inc),
+//     which keeps the two waves of each SIMD in lock-step so that their
+//     full-rate add/xor instructions pair up;
+//   * the XOR result leaves through the same swizzled slice, lane-contiguously;
+//   * Poly1305 is fed from the ciphertext registers themselves: the wave's 64
+//     lanes hold 256 consecutive 16-byte ciphertext chunks, which are the B
+//     operands of four v_mfma_i32_32x32x32_i8 per iteration (see "MAC" below).
+//
+// MAC.  The reference evaluates h = sum_b v_b r^(B - b) over the 16-byte
+// blocks of ad || le64(|ad|) || ct || le64(|ct|) (chacha20_poly1305.rs:19-42,
+// poly1305.rs:207-228).  Ciphertext chunk m (bytes 16 m .. 16 m + 15) starts
+// at stream offset o + 16 m, o = |ad| + 8 = 16 beta + sigma, so its byte a' has
+// weight 2^(8 (sigma + a')) r^(E(m) + 1) when sigma + a' < 16 and
+// 2^(8 (sigma + a' - 16)) r^E(m) otherwise, with E(m) = B - beta - 1 - m.
+// Chunk m = 256 j + 128 h + 4 q + i (iteration j, lane 32 h + q, chunk i of
+// the lane's block) factors as E(m) = 4 (31 - q) + e(j, h, i),
+// e = 128 (1 - h) + 256 (3 - j) + (4 - i) + delta.  Each MFMA step (j, i) then
+// computes D[c][q] += sum_{h, a'} T[c][(h, a')] (byte - 128), where column q
+// is the lane's chunk and row c a base-256 digit position: T holds the signed
+// digits of r^(e + 1) and r^e, shifted by sigma + a' (a Toeplitz band).  The
+// eight powers per step, r^(128 k + 1 + delta + u) (k = 0..7, u = 0..4), are
+// built once per record as 48-byte digit lines in LDS; a lane reads its
+// 16-byte T fragment as two unaligned windows of two adjacent lines.  |D| <
+// 2^23, so with the accumulator seeded at 2^24 every entry is a positive
+// 25-bit integer.  At the end each lane assembles its 16 entries exactly,
+// X = sum_r D[c_r][q] 2^(8 c_r), reduces it mod 2^130 - 5, multiplies by
+// W = r^(4 (31 - q)) (times 2^32 for the upper half-wave) and a DPP sum adds
+// the 64 terms.  The keying kernel supplies the per-record constant ctot:
+// the AD / length blocks, the pad bits, the i8 bias and the seed.  Every step
+// is exact arithmetic mod p, so tags equal the reference's bit for bit
+// (tests/test_wpr_mac_model.py pins this decomposition against the CPU
+// restatement of poly1305.rs).
+#include "sg_internal.h"
+#include "sg_device.h"
+#include "sg_chacha_grp.inc"  // grouped ChaCha20 double round (tools/gen_chacha_grp.py --product)
+
+#include <stdint.h>
+#include <stdlib.h>
+
+namespace sg {
+namespace {
+
+using namespace dev;
+
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x16 __attribute__((ext_vector_type(16)));
+
+constexpr uint32_t kWprWaves = 8;           // records per 512-thread workgroup
+constexpr uint32_t kWprChunk = 4096;        // bytes per wave iteration
+constexpr uint32_t kWprLines = 40;          // T digit lines per record
+constexpr uint32_t kWprLineBytes = 48;
+constexpr uint32_t kWprLinesOff = 2 * kWprChunk;  // two chunk buffers, then the T lines
+constexpr uint32_t kWprWaveLds = 2 * kWprChunk + kWprLines * kWprLineBytes + 64;  // 10176: two workgroups per CU
+constexpr uint32_t kWprKeyThreads = 64;
+constexpr uint32_t kWprKeyStride = 81;      // LDS words per record and half
+
+// Geometry of the MAC stream ad || le64(|ad|) || ct || le64(n) for n = 2^14.
+struct WprGeom {
+    uint32_t o, sigma, beta, B, rem, delta;
+};
+__device__ __forceinline__ WprGeom wpr_geom(uint32_t adlen) {
+    WprGeom g;
+    g.o = adlen + 8u;
+    g.sigma = g.o & 15u;
+    g.beta = g.o >> 4;
+    const uint32_t L = adlen + 16u + kWprN;
+    g.B = (L + 15u) >> 4;
+    g.rem = L - 16u * (g.B - 1u);
+    g.delta = g.B - g.beta - 1u - 1024u;  // 0 or 1
+    return g;
+}
+
+// bytes >= lo of a little-endian word set: mask of the bytes whose index
+// (4 w + byte) is >= lo
+__device__ __forceinline__ uint32_t bytes_from(uint32_t w, uint32_t lo) {
+    if (lo <= 4u * w) return 0xffffffffu;
+    if (lo >= 4u * w + 4u) return 0u;
+    return 0xffffffffu << (8u * (lo - 4u * w));
+}
+
+// p - (2^24 * sum_{c<32} 2^(8c) mod p) in radix 2^26: the seed of the 32 x 32
+// accumulator, negated (tests/test_wpr_mac_model.py: CJ)
+constexpr uint32_t kCJ0 = 0x1bd2d2bu, kCJ1 = 0x36f6f6fu, kCJ2 = 0x3dbdbdbu, kCJ3 = 0x2f6f6f6u, kCJ4 = 0x1bdbdbdu;
+
+// ---------------------------------------------------------------------------
+// Keying pre-pass: one lane per record, 64 records per wave, the 160-word
+// record (sg_internal.h, kW*) staged in LDS by halves and stored coalesced.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void wpr_flush_half(const KParams& p, uint32_t rec0, uint32_t half, const uint32_t* stage,
+                                               uint32_t lane) {
+    const uint32_t nrec = p.count - rec0 < kWprKeyThreads ? p.count - rec0 : kWprKeyThreads;
+    const uint32_t nvec = nrec * 20u;  // 80 words = 20 x 16 B per record and half
+    for (uint32_t v = lane; v < nvec; v += kWprKeyThreads) {
+        const uint32_t rr = v / 20u, c = v - rr * 20u;
+        const uint32_t* src = stage + rr * kWprKeyStride + 4u * c;
+        st16(p.ws + (uint64_t)(rec0 + rr) * kWprRecWords + 80u * half + 4u * c, u32x4{src[0], src[1], src[2], src[3]});
+    }
+}
+
+template <bool OPEN>
+__global__ __launch_bounds__(64) void sg_wpr_keying_kernel(const KParams p) {
+    __shared__ uint32_t stage[kWprKeyThreads * kWprKeyStride];
+    const uint32_t lane = threadIdx.x;
+    const uint32_t rec0 = blockIdx.x * kWprKeyThreads;
+    const uint32_t rec = rec0 + lane;
+    uint32_t* st = stage + lane * kWprKeyStride;
+    const uint32_t adlen = p.tls ? 13u : p.ad_len;
+    const WprGeom G = wpr_geom(adlen);
+
+    F26 r = f26_zero();
+    uint32_t s[4] = {0u, 0u, 0u, 0u};
+    RecKey rk = {};
+    const bool act = rec < p.count;
+    if (act) {
+        rk = record_key(p, rec);
+        uint32_t ks[16];
+        chacha_block(ks, rk.k, 0u, rk.n14, rk.n15);  // block 0 -> poly key (chacha20_poly1305.rs:50,75)
+        // r = clamp(pk[0..16]) (poly1305.rs:197-203), s = pk[16..32] (chacha20_poly1305.rs:32-39)
+        r = words_to_f26(ks[0] & 0x0fffffffu, ks[1] & 0x0ffffffcu, ks[2] & 0x0ffffffcu, ks[3] & 0x0ffffffcu, 0u);
+        s[0] = ks[4]; s[1] = ks[5]; s[2] = ks[6]; s[3] = ks[7];
+    }
+
+    // ---- second half: lo[b] = R^b, hi[h][a] = 2^(32 h) R^(8 a) (R = r^4) ----
+    const F26 r2 = fmul(r, r), R = fmul(r2, r2);
+    F26 x = f26_one(), sum_lo = f26_zero();
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+        store_f26(st + (kWLo - 80u) + 5u * b, x);
+        sum_lo = f26_add(sum_lo, x);
+        x = fmul(x, R);
+    }
+    const F26 R8 = x;
+    F26 y = f26_one(), sum_hi = f26_zero();
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+        store_f26(st + (kWHi - 80u) + 5u * a, y);
+        store_f26(st + (kWHi - 80u) + 20u + 5u * a, mul_add(y, 0u, 64u, 0u, 0u, 0u, f26_zero()));  // * 2^32
+        sum_hi = f26_add(sum_hi, y);
+        y = fmul(y, R8);
+    }
+    const F26 T = y;  // R^32 = r^128
+    __syncthreads();
+    wpr_flush_half(p, rec0, 1u, stage, lane);
+    __syncthreads();
+
+    // ---- first half: s, ctot, rd[u] = r^(1 + delta + u), tk[k] = T^k ----
+    st[kWS + 0] = s[0]; st[kWS + 1] = s[1]; st[kWS + 2] = s[2]; st[kWS + 3] = s[3];
+    const F26 r3 = fmul(r2, r), r5 = fmul(R, r), r6 = fmul(R, r2);
+    const bool d1 = G.delta != 0u;
+    const F26 pw[6] = {r, r2, r3, R, r5, r6};
+#pragma unroll
+    for (int u = 0; u < 5; ++u) store_f26(st + kWRd + 5u * u, d1 ? pw[u + 1] : pw[u]);
+    const F26 rd0 = d1 ? r2 : r;        // r^(1 + delta)
+    const F26 rdel = d1 ? r : f26_one();  // r^delta
+    F26 t = f26_one(), sum_t = f26_zero();
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        store_f26(st + kWTk + 5u * k, t);
+        sum_t = f26_add(sum_t, t);
+        t = fmul(t, T);
+    }
+    const F26 T8 = t;  // r^1024
+
+    // geometric sums: SW = sum_{u<32} R^u, g = G(1024) = (r + r^2 + r^3 + r^4) SW sum_k T^k
+    const F26 SW = fmul(carry1(sum_hi), carry1(sum_lo));
+    const F26 G4 = carry1(f26_add(f26_add(r, r2), f26_add(r3, R)));
+    const F26 g = fmul(fmul(G4, SW), carry1(sum_t));
+    // pads (poly1305.rs:224-225): 2^128 sum_{b < B-1} r^(B-b) + 2^(8 rem) r
+    //   = 2^128 G(B) + (2^(8 rem) + p - 2^128) r,  G(B) = G(1024) + r^1024 G(B - 1024)
+    const F26 GB = fmul_add(T8, geo_sum(r, G.B - 1024u), g);
+    F26 pads = mul_add(GB, 0u, 0u, 0u, 0u, 1u << 24, f26_zero());
+    {
+        F26 cf = F26{0x3fffffbu, 0x3ffffffu, 0x3ffffffu, 0x3ffffffu, 0x2ffffffu};  // p - 2^128
+        const uint32_t bit = 8u * G.rem, li = bit / 26u, v = 1u << (bit - 26u * li);
+        cf.v0 += li == 0u ? v : 0u;
+        cf.v1 += li == 1u ? v : 0u;
+        cf.v2 += li == 2u ? v : 0u;
+        cf.v3 += li == 3u ? v : 0u;
+        cf.v4 += li == 4u ? v : 0u;
+        pads = fmul_add(cf, r, pads);
+    }
+    // i8 bias: 128 sum over the ciphertext bytes of their weights
+    //   = r^delta G(1024) (A1 r + A2),  A1 = sum_{k=sigma}^{15} 128 2^(8k),  A2 = sum_{k<sigma} 128 2^(8k)
+    F26 bias;
+    {
+        uint32_t a1[4], a2[4];
+#pragma unroll
+        for (uint32_t w = 0; w < 4; ++w) {
+            const uint32_t m = bytes_from(w, G.sigma);
+            a1[w] = 0x80808080u & m;
+            a2[w] = 0x80808080u & ~m;
+        }
+        const F26 A1 = words_to_f26(a1[0], a1[1], a1[2], a1[3], 0u);
+        const F26 A2 = words_to_f26(a2[0], a2[1], a2[2], a2[3], 0u);
+        bias = fmul(fmul(g, fmul_add(A1, r, A2)), rdel);
+    }
+    // accumulator seed: -(2^24 sum_c 2^(8c)) SW
+    const F26 seed = mul_add(SW, kCJ0, kCJ1, kCJ2, kCJ3, kCJ4, f26_zero());
+    // prefix ad || le64(|ad|) (stream bytes < o) as blocks 0..beta: Horner, then r^(B - beta) = r^1024 r^(1 + delta)
+    F26 hp = f26_zero();
+    if (act) {
+        for (uint32_t b = 0; b <= G.beta; ++b) {
+            uint32_t w[4] = {0u, 0u, 0u, 0u};
+            for (uint32_t i = 0; i < 16u; ++i) {
+                const uint32_t pos = 16u * b + i;
+                if (pos < G.o) w[i >> 2] |= (uint32_t)prefix_byte(p, rec, rk.seq, kWprN, adlen, pos) << (8u * (i & 3u));
+            }
+            hp = fmul_add(hp, r, words_to_f26(w[0], w[1], w[2], w[3], 0u));
+        }
+    }
+    const F26 prefix = fmul(fmul(hp, T8), rd0);
+    // suffix le64(n) at stream offset o + n = 16 (beta + 1024) + sigma: n 2^(8 sigma) split at 2^128
+    F26 suffix;
+    {
+        const uint32_t wi = G.sigma >> 2, bs = 8u * (G.sigma & 3u);
+        const uint64_t v = (uint64_t)kWprN << bs;
+        uint32_t w[5] = {0u, 0u, 0u, 0u, 0u};
+#pragma unroll
+        for (uint32_t i = 0; i < 4; ++i) {
+            if (i == wi) {
+                w[i] = (uint32_t)v;
+                w[i + 1] = (uint32_t)(v >> 32);
+            }
+        }
+        suffix = fmul_add(words_to_f26(w[0], w[1], w[2], w[3], 0u), rd0, fmul(F26{w[4], 0u, 0u, 0u, 0u}, rdel));
+    }
+    const F26 ctot = carry1(f26_add(f26_add(f26_add(pads, bias), f26_add(seed, prefix)), suffix));
+    store_f26(st + kWCtot, ctot);
+    __syncthreads();
+    wpr_flush_half(p, rec0, 0u, stage, lane);
+}
+
+// ---------------------------------------------------------------------------
+// The record kernel.
+// ---------------------------------------------------------------------------
+// Four LDS-DMA loads (global_load_lds_dwordx4, 1 KiB each) of one 4 KiB chunk:
+// instruction k writes LDS bytes [l0 + 1024 k, +1024) from each lane's
+// g0 + 1024 k.  hipcc does not count these loads: the kernel waits for them
+// with its own s_waitcnt vmcnt.
+__device__ __forceinline__ void dma_chunk(uint32_t l0, const uint8_t* g0) {
+    const uint8_t* g1 = g0 + 1024;
+    const uint8_t* g2 = g0 + 2048;
+    const uint8_t* g3 = g0 + 3072;
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %5\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
+        "s_mov_b32 m0, %6\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, off\n\t"
+        "s_mov_b32 m0, %7\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %3, off\n\t"
+        "s_mov_b32 m0, %8\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %4, off\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(g0), "v"(g1), "v"(g2), "v"(g3), "s"(l0), "s"(uniform(l0 + 1024u)), "s"(uniform(l0 + 2048u)), "s"(uniform(l0 + 3072u))
+        : "memory");
+}
+
+// X = sum_m Y_m 2^(64 m) < 2^242 (eight words) -> F26 with limb 4 < 2^27.
+__device__ __forceinline__ F26 reduce_words8(const uint32_t w[8]) {
+    // y = (X mod 2^130) + 5 (X >> 130) < 2^131, then once more
+    uint64_t t = (uint64_t)__builtin_amdgcn_alignbit(w[5], w[4], 2) * 5u + w[0];
+    const uint32_t y0 = (uint32_t)t;
+    t = (uint64_t)__builtin_amdgcn_alignbit(w[6], w[5], 2) * 5u + w[1] + (t >> 32);
+    const uint32_t y1 = (uint32_t)t;
+    t = (uint64_t)__builtin_amdgcn_alignbit(w[7], w[6], 2) * 5u + w[2] + (t >> 32);
+    const uint32_t y2 = (uint32_t)t;
+    t = (uint64_t)(w[7] >> 2) * 5u + w[3] + (t >> 32);
+    const uint32_t y3 = (uint32_t)t;
+    t = (uint64_t)(w[4] & 3u) + (t >> 32);                     // y = y0..y3 + t 2^128
+    const uint64_t u = (uint64_t)(uint32_t)(t >> 2) * 5u + y0;  // (y mod 2^130) + 5 (y >> 130)
+    uint32_t c;
+    const uint32_t z1 = addc(y1, (uint32_t)(u >> 32), 0u, &c);
+    const uint32_t z2 = addc(y2, 0u, c, &c);
+    const uint32_t z3 = addc(y3, 0u, c, &c);
+    const uint32_t z4 = ((uint32_t)t & 3u) + c;  // <= 4
+    F26 f = words_to_f26((uint32_t)u, z1, z2, z3, 0u);
+    f.v4 += z4 << 24;
+    return f;
+}
+
+// Scalar loads of wave-uniform inputs (key table, key index, sequence numbers,
+// explicit nonces, the received tag): the constant address space makes hipcc
+// emit s_load (counted on lgkmcnt), so no compiler-counted vector load ever
+// waits behind the kernel's own LDS-DMA queue.
+typedef const __attribute__((address_space(4))) uint32_t* cu32p;
+__device__ __forceinline__ uint32_t cload(const void* base, uint64_t word) {
+    return ((cu32p)(uintptr_t)base)[word];
+}
+
+// One 16-byte LDS-DMA per lane: LDS [l0 + 16 lane, +16) <- g (lanes with exec set).
+__device__ __forceinline__ void dma_one(uint32_t l0, const void* g) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(g), "s"(l0)
+                 : "memory");
+}
+
+template <bool OPEN, bool TLS>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) void sg_wpr_kernel(const KParams p) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const uint32_t wave = uniform(threadIdx.x >> 6), lane = threadIdx.x & 63u;
+    uint8_t* buf = lds + wave * kWprWaveLds;
+    uint8_t* lines = buf + kWprLinesOff;  // also the landing area of the record's keying table
+    const uint32_t lds_wave = uniform((uint32_t)(uintptr_t)buf);
+    const uint32_t lds_lines = uniform(lds_wave + kWprLinesOff);
+    const uint32_t hh = lane >> 5, q = lane & 31u;
+    const uint32_t adlen = TLS ? 13u : p.ad_len;
+    const uint32_t sigma = (adlen + 8u) & 15u;
+    // T fragment byte a' comes from the V window for a' < 16 - sigma, else from P
+    const uint32_t nv = 16u - sigma;
+    const u32x4 vmask = {~bytes_from(0u, nv), ~bytes_from(1u, nv), ~bytes_from(2u, nv), ~bytes_from(3u, nv)};
+    // LDS swizzle: 16-byte unit 4 t + c of a chunk lives at 4 t + (c ^ ((t >> 2) & 3))
+    const uint32_t wunit = (lane & ~3u) | ((lane ^ (lane >> 4)) & 3u);  // unit of global position 64 k + lane
+    const uint32_t xq = (lane >> 2) & 3u;
+    const uint32_t ngroups = (p.count + kWprWaves - 1u) / kWprWaves;
+
+    // Chunk c of a record is fetched by LDS-DMA into buffer c & 1, one chunk
+    // ahead: lane l of DMA instruction k lands at LDS unit 64 k + l and reads
+    // global unit 64 k + wunit(l), so LDS unit phi(g) holds global unit g
+    // (phi = wunit within each 64-unit piece, an involution).  The record's
+    // keying table (640 B) is fetched into the line area the same way.  The
+    // only vector-memory operations of the kernel are these DMAs and the
+    // output stores, so the waits below count exactly.
+    auto dma_chunk_of = [&](uint32_t rec, uint32_t c) {
+        dma_chunk(lds_wave + kWprChunk * (c & 1u), p.in + p.in_stride * rec + kWprChunk * c + 16u * wunit);
+    };
+    auto dma_table_of = [&](uint32_t rec) {
+        if (lane < kWprRecWords / 4u) dma_one(lds_lines, p.ws + (uint64_t)rec * kWprRecWords + 4u * lane);
+    };
+    uint32_t g = blockIdx.x;
+    if (g < ngroups && g * kWprWaves + wave < p.count) {
+        dma_chunk_of(g * kWprWaves + wave, 0u);
+        dma_table_of(g * kWprWaves + wave);
+    }
+    bool first = true;
+
+    for (; g < ngroups; g += gridDim.x) {
+        const uint32_t rec = g * kWprWaves + wave;
+        const bool active = rec < p.count;  // an inactive wave still runs every round and barrier
+        const uint32_t recl = rec < p.count ? rec : p.count - 1u;
+        const uint32_t gn = g + gridDim.x, nrec = gn * kWprWaves + wave;
+        const bool next = gn < ngroups && nrec < p.count;
+        uint8_t* out = p.out + p.out_stride * recl;
+        // key, nonce (chacha20.rs:25-51; TLS: be64(seq), tls.rs:103), received tag
+        uint32_t kw[8];
+        {
+            const uint32_t ki = p.key_index ? cload(p.key_index, recl) : 0u;
+#pragma unroll
+            for (uint32_t i = 0; i < 8u; ++i) kw[i] = cload(p.keys, 8ull * ki + i);
+        }
+        uint32_t n14, n15;
+        if constexpr (TLS) {
+            uint64_t seq = p.seq0 + recl;
+            if (p.seq) seq = (uint64_t)cload(p.seq, 2ull * recl) | ((uint64_t)cload(p.seq, 2ull * recl + 1u) << 32);
+            n14 = bswap32((uint32_t)(seq >> 32));
+            n15 = bswap32((uint32_t)seq);
+        } else {
+            n14 = cload(p.nonces, 2ull * recl);
+            n15 = cload(p.nonces, 2ull * recl + 1u);
+        }
+        uint32_t rx[4] = {0u, 0u, 0u, 0u};
+        if constexpr (OPEN) {  // the received tag (chacha20_poly1305.rs:72-73)
+            const uint8_t* tg = p.in + p.in_stride * recl + kWprN;
+            rx[0] = cload(tg, 0); rx[1] = cload(tg, 1); rx[2] = cload(tg, 2); rx[3] = cload(tg, 3);
+        }
+
+        // ---- the keying table has landed (it was followed by the previous
+        // record's four chunk stores and its tag / status store)
+        if (first) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+        first = false;
+        wave_lds_sync();
+        const uint32_t* tab = reinterpret_cast<const uint32_t*>(lines);
+        // row weight W = 2^(32 hh) r^(4 (31 - q)) = hi[hh][a] lo[b], 31 - q = 8 a + b
+        const uint32_t e = 31u - q;
+        const F26 W = fmul(load_f26(tab + kWHi + 20u * hh + 5u * (e >> 3)), load_f26(tab + kWLo + 5u * (e & 7u)));
+        const F26 ctot = {uniform(tab[kWCtot + 0]), uniform(tab[kWCtot + 1]), uniform(tab[kWCtot + 2]),
+                          uniform(tab[kWCtot + 3]), uniform(tab[kWCtot + 4])};
+        const uint32_t sk[4] = {uniform(tab[kWS + 0]), uniform(tab[kWS + 1]), uniform(tab[kWS + 2]),
+                                uniform(tab[kWS + 3])};
+        // ---- T digit lines: line l = 5 k + u holds r^(128 k + 1 + delta + u) as
+        // 17 signed base-256 digits, digit i at byte 47 - sigma - i, zeros elsewhere
+        F26 lv = f26_zero();
+        if (lane < kWprLines) {
+            const uint32_t k = lane / 5u, u = lane - 5u * k;
+            lv = fmul(load_f26(tab + kWRd + 5u * u), load_f26(tab + kWTk + 5u * k));
+        }
+        wave_lds_sync();  // every table read is done before the lines overwrite it
+        if (lane < kWprLines) {
+            const F26 v = canonical(lv);
+            uint32_t c;  // digits = the bytes of v + 0x80..80, each ^ 0x80
+            uint32_t d[5];
+            d[0] = addc(v.v0 | (v.v1 << 26), 0x80808080u, 0u, &c) ^ 0x80808080u;
+            d[1] = addc((v.v1 >> 6) | (v.v2 << 20), 0x80808080u, c, &c) ^ 0x80808080u;
+            d[2] = addc((v.v2 >> 12) | (v.v3 << 14), 0x80808080u, c, &c) ^ 0x80808080u;
+            d[3] = addc((v.v3 >> 18) | (v.v4 << 8), 0x80808080u, c, &c) ^ 0x80808080u;
+            d[4] = ((v.v4 >> 24) + 0x80u + c) ^ 0x80u;
+            uint8_t* ln = lines + kWprLineBytes * lane;
+            st16(ln, u32x4{0u, 0u, 0u, 0u});
+            st16(ln + 16, u32x4{0u, 0u, 0u, 0u});
+            st16(ln + 32, u32x4{0u, 0u, 0u, 0u});
+#pragma unroll
+            for (uint32_t i = 0; i < 17u; ++i) ln[47u - sigma - i] = (uint8_t)(d[i >> 2] >> (8u * (i & 3u)));
+        } else if (lane == kWprLines) {
+            st16(lines + kWprLines * kWprLineBytes, u32x4{0u, 0u, 0u, 0u});
+        }
+        wave_lds_sync();
+
+        i32x16 acc;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[i] = 1 << 24;
+
+#pragma unroll
+        for (uint32_t j = 0; j < 4u; ++j) {
+            // chunk j has landed in buffer j & 1 (j >= 1: it was followed by the
+            // four stores of chunk j - 1; j = 0: waited for with the table)
+            if (j > 0u) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            wave_lds_sync();
+            uint8_t* cb = buf + kWprChunk * (j & 1u);
+            u32x4 D[4];
+#pragma unroll
+            for (uint32_t i = 0; i < 4u; ++i) D[i] = ld16(cb + 16u * (4u * lane + (i ^ xq)));
+            // prefetch the next chunk into the other buffer (its last reader, the
+            // read-out of chunk j - 1, has completed: its data was stored)
+            if (j < 3u) {
+                if (active) dma_chunk_of(rec, j + 1u);
+            } else if (next) {
+                dma_chunk_of(nrec, 0u);
+            }
+
+            // keystream block 64 j + lane + 1 (chacha20_poly1305.rs:52), lock-step rounds
+            const uint32_t ctr = 64u * j + lane + 1u;
+            uint32_t x[16] = {kSigma0, kSigma1, kSigma2, kSigma3, kw[0], kw[1], kw[2], kw[3],
+                              kw[4],   kw[5],   kw[6],   kw[7],   ctr,   0u,    n14,   n15};
+#pragma unroll 1
+            for (int r = 0; r < 10; ++r)
+                asm volatile(SG_CHACHA_DR_NB1_BAR1
+                             : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]),
+                               "+v"(x[7]), "+v"(x[8]), "+v"(x[9]), "+v"(x[10]), "+v"(x[11]), "+v"(x[12]), "+v"(x[13]),
+                               "+v"(x[14]), "+v"(x[15]));
+            // feed-forward (chacha20.rs:104-106), XOR (chacha20.rs:143-153), and the
+            // MAC step of each chunk on the ciphertext: received (open) or just
+            // produced (seal).  Step (j, i): T fragment = the V window of line
+            // iv = 5 k + 4 - i for bytes a' < 16 - sigma, else the P window of line iv - 1
+            const u32x4 ks[4] = {u32x4{x[0] + kSigma0, x[1] + kSigma1, x[2] + kSigma2, x[3] + kSigma3},
+                                 u32x4{x[4] + kw[0], x[5] + kw[1], x[6] + kw[2], x[7] + kw[3]},
+                                 u32x4{x[8] + kw[4], x[9] + kw[5], x[10] + kw[6], x[11] + kw[7]},
+                                 u32x4{x[12] + ctr, x[13], x[14] + n14, x[15] + n15}};
+            const uint32_t kk = (1u - hh) + 2u * (3u - j);
+            u32x4 O[4];
+#pragma unroll
+            for (uint32_t i = 0; i < 4u; ++i) {
+                O[i] = D[i] ^ ks[i];
+                const uint32_t iv = 5u * kk + 4u - i;
+                const u32x4 V = ldu16(lines + kWprLineBytes * iv + 47u - q);
+                const u32x4 P = ldu16(lines + kWprLineBytes * iv - 17u - q);
+                const u32x4 f = (V & vmask) | (P & ~vmask);
+                acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(__builtin_bit_cast(i32x4, f),
+                                                             __builtin_bit_cast(i32x4, (OPEN ? D[i] : O[i]) ^ 0x80808080u),
+                                                             acc, 0, 0, 0);
+            }
+            if (j == 3u && next) {  // the lines are read: the next record's keying table may land
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                wave_lds_sync();
+                dma_table_of(nrec);
+            }
+
+            // the output leaves through the same slice, lane-contiguously
+#pragma unroll
+            for (uint32_t i = 0; i < 4u; ++i) st16(cb + 16u * (4u * lane + (i ^ xq)), O[i]);
+            wave_lds_sync();
+            const u32x4 o0 = ld16(cb + 16u * wunit), o1 = ld16(cb + 1024u + 16u * wunit);
+            const u32x4 o2 = ld16(cb + 2048u + 16u * wunit), o3 = ld16(cb + 3072u + 16u * wunit);
+            if (active) {
+                uint8_t* dst = out + kWprChunk * j + 16u * lane;
+                st16(dst, o0);
+                st16(dst + 1024, o1);
+                st16(dst + 2048, o2);
+                st16(dst + 3072, o3);
+            }
+            wave_lds_sync();
+        }
+
+        // ---- assemble X = sum_r D[c_r][q] 2^(8 c_r - 32 hh), c_r = (r & 3) + 8 (r >> 2) + 4 hh
+        uint32_t xw[8];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            uint64_t yv = (uint64_t)(uint32_t)acc[4 * m + 1] * 256u + (uint32_t)acc[4 * m];
+            yv += (uint64_t)(uint32_t)acc[4 * m + 2] * 65536u;
+            yv += (uint64_t)(uint32_t)acc[4 * m + 3] * 16777216u;
+            xw[2 * m] = (uint32_t)yv;
+            xw[2 * m + 1] = (uint32_t)(yv >> 32);
+        }
+        F26 f = fmul(reduce_words8(xw), W);
+        {  // sum the 64 lane terms into lane 63: row_shr 1, 2, 4, 8, row_bcast:15, carry, row_bcast:31
+            auto level = [&](auto dpp) {
+                f.v0 += dpp(f.v0); f.v1 += dpp(f.v1); f.v2 += dpp(f.v2); f.v3 += dpp(f.v3); f.v4 += dpp(f.v4);
+            };
+            level([](uint32_t v) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true); });
+            level([](uint32_t v) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true); });
+            level([](uint32_t v) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, true); });
+            level([](uint32_t v) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, true); });
+            level([](uint32_t v) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xf, 0xf, true); });
+            f = carry1(f);
+            level([](uint32_t v) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xf, 0xf, true); });
+        }
+        auto lane63 = [](uint32_t v) { return (uint32_t)__builtin_amdgcn_readlane((int)v, 63); };
+        const F26 fs = {lane63(f.v0) + ctot.v0, lane63(f.v1) + ctot.v1, lane63(f.v2) + ctot.v2,
+                        lane63(f.v3) + ctot.v3, lane63(f.v4) + ctot.v4};
+        uint32_t tw[4];
+        tag_words(fs, sk, tw);
+        if (active && lane == 0u) {
+            if constexpr (!OPEN) {
+                st16(out + kWprN, u32x4{tw[0], tw[1], tw[2], tw[3]});  // ct || tag (chacha20_poly1305.rs:55)
+            } else {
+                // constant-time compare: diff |= a ^ b over all 16 bytes (chacha20_poly1305.rs:84-87)
+                const uint32_t diff = (rx[0] ^ tw[0]) | (rx[1] ^ tw[1]) | (rx[2] ^ tw[2]) | (rx[3] ^ tw[3]);
+                p.status[rec] = diff != 0u ? 1u : 0u;
+            }
+        }
+    }
+}
+
+int g_cus[64];  // CUs per device ordinal (0: not read yet)
+
+}  // namespace
+
+hipError_t launch_wpr(const KParams& p, bool open, hipStream_t s, hipEvent_t ev_keyed, hipEvent_t ev_start) {
+    const uint32_t kgrid = (p.count + kWprKeyThreads - 1u) / kWprKeyThreads;
+    if (open)
+        hipLaunchKernelGGL((sg_wpr_keying_kernel<true>), dim3(kgrid), dim3(kWprKeyThreads), 0, s, p);
+    else
+        hipLaunchKernelGGL((sg_wpr_keying_kernel<false>), dim3(kgrid), dim3(kWprKeyThreads), 0, s, p);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    if (ev_keyed && (e = hipEventRecord(ev_keyed, s)) != hipSuccess) return e;
+    if (ev_start && (e = hipEventRecord(ev_start, s)) != hipSuccess) return e;
+    int dev = 0;
+    if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
+    int cus = dev >= 0 && dev < 64 ? __atomic_load_n(&g_cus[dev], __ATOMIC_RELAXED) : 0;
+    if (cus <= 0) {
+        if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return e;
+        if (dev >= 0 && dev < 64) __atomic_store_n(&g_cus[dev], cus, __ATOMIC_RELAXED);
+    }
+    const uint32_t ngroups = (p.count + kWprWaves - 1u) / kWprWaves;
+    uint32_t grid = 2u * (uint32_t)cus;  // two workgroups (16 waves) per CU
+    if (grid > ngroups) grid = ngroups;
+    const size_t lds = kWprWaves * kWprWaveLds;
+#define SG_WPR_LAUNCH(O, T) hipLaunchKernelGGL((sg_wpr_kernel<O, T>), dim3(grid), dim3(512), lds, s, p)
+    if (open) {
+        if (p.tls) SG_WPR_LAUNCH(true, true); else SG_WPR_LAUNCH(true, false);
+    } else {
+        if (p.tls) SG_WPR_LAUNCH(false, true); else SG_WPR_LAUNCH(false, false);
+    }
+#undef SG_WPR_LAUNCH
+    return hipGetLastError();
+}
+
+#ifndef SG_WPR_DEFAULT
+#define SG_WPR_DEFAULT 1
+#endif
+static int g_wpr = -1;  // -1: not read from the environment yet
+bool wpr_enabled() {
+    if (__atomic_load_n(&g_wpr, __ATOMIC_ACQUIRE) < 0) {
+        const char* e = getenv("SG_LOCKSTEP");
+        int expect = -1;
+        __atomic_compare_exchange_n(&g_wpr, &expect, e ? (e[0] == '1' ? 1 : 0) : (SG_WPR_DEFAULT ? 1 : 0), false,
+                                    __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE);
+    }
+    return __atomic_load_n(&g_wpr, __ATOMIC_ACQUIRE) == 1;
+}
+int set_wpr(int enable) {
+    const int prev = wpr_enabled() ? 1 : 0;
+    if (enable >= 0) __atomic_store_n(&g_wpr, enable ? 1 : 0, __ATOMIC_RELEASE);
+    return prev;
+}
+
+const char* wpr_kernel_config() {
+    return "sg_wpr_kernel v12: full 16 KiB records, one wave per record (8 per 512-thread workgroup, persistent "
+           "2 per CU), 4 KiB chunks prefetched lane-contiguously and staged through an XOR-swizzled LDS slice, "
+           "lock-step grouped ChaCha20 rounds (s_barrier per rotate group), Poly1305 as 16 v_mfma_i32_32x32x32_i8 "
+           "per record fed from the ciphertext registers (Toeplitz digit lines of r^(128k+d) in LDS), exact "
+           "per-lane assembly, W = r^(4(31-q)) scaling, DPP sum; keying pre-pass with the constant term";
+}
+
+}  // namespace sg

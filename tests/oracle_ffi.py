@@ -63,6 +63,8 @@ class Oracle:
         L.so_open_batch_tls.argtypes = [u8p, C.c_uint64, C.c_void_p, C.c_size_t, C.c_size_t, C.c_void_p,
                                         C.c_void_p, C.c_int]
         L.so_open_batch_tls.restype = C.c_size_t
+        L.so_tag_fold_tls.argtypes = [u8p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_size_t, C.c_size_t, C.c_int,
+                                      C.c_void_p]
         self.L = L
 
     # --- primitives
@@ -119,6 +121,12 @@ class Oracle:
         st = C.create_string_buffer(max(count, 1))
         bad = self.L.so_open_batch_tls(key, seq0, ct, n, count, out, st, threads)
         return bad, out.raw[:n * count], st.raw[:count]
+
+    def tag_fold_tls(self, key: bytes, seq0: int, seed: int, j0: int, n: int, count: int, threads: int = 1) -> bytes:
+        """XOR of the tags of count sealed fill-rule records (never materialised)."""
+        out = C.create_string_buffer(16)
+        self.L.so_tag_fold_tls(key, seq0, seed, j0, n, count, threads, out)
+        return out.raw
 
 
 _oracle = None

@@ -109,6 +109,22 @@ def test_no_cpu_fallback_in_product():
         assert "import oracle" not in text and "oracle_ffi" not in text, py
 
 
+def test_product_sources_carry_no_wrong_output_switches():
+    """The timing-experiment switches of round 1 that skipped the MAC or the
+    rounds (tags wrong) are not in the product sources, and _build refuses
+    them (SG_LS_NO*, SG_LS_COMPILED, SG_EXP_*, SG_MAC_GLOBAL_A)."""
+    from suruga_amd import _build
+
+    for src in _build.HIP_DEPS:
+        text = src.read_text()
+        for tok in ("SG_LS_NOMAC", "SG_LS_NOROUNDS", "SG_LS_COMPILED", "SG_EXP_", "SG_MAC_GLOBAL_A", "SG_MACX"):
+            assert tok not in text, (src.name, tok)
+    with pytest.raises(ValueError):
+        _build.build_library(out=ROOT / "build_variant_never_written.so", defines=["-DSG_LS_NOMAC=1"])
+    with pytest.raises(ValueError):
+        _build.build_library(defines=["-DSG_SALU_PRE=0"])  # product lib: no switches at all
+
+
 def test_missing_library_fails_loudly(tmp_path):
     """A missing HIP library is an ImportError naming the build step, never a
     silent CPU path (the loader is the product's only way to the kernels)."""

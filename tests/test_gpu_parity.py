@@ -416,12 +416,9 @@ def test_length_sweep_every_mac_geometry(gpu, oracle, adlen):
 
 
 # ---------------------------------------------------------------------------
-# lock-step kernel (uniform batches of 8 KiB < n <= 16 KiB, sg_aead_ls_kernel)
+# wave-per-record kernel (uniform batches of full 16 KiB records, sg_wpr.hip)
 # ---------------------------------------------------------------------------
-LS_LENGTHS = [8193, 8200, 9000, 10240, 12287, 12288, 12289, 16320, 16321, 16383, 16384]
-
-
-@pytest.fixture(params=[1, 0], ids=["lockstep", "sizeclass"])
+@pytest.fixture(params=[1, 0], ids=["wpr", "sizeclass"])
 def kernel_form(request, gpu):
     from suruga_amd import _native as N
 
@@ -432,51 +429,96 @@ def kernel_form(request, gpu):
     lib.sg_set_lockstep(prev)
 
 
-@pytest.mark.parametrize("adlen", [13, 0, 7, 255])
-def test_lockstep_uniform_geometries(gpu, oracle, kernel_form, adlen):
-    """Uniform batches over every MAC geometry the lock-step kernel takes
-    (k = 3 or 5 blocks per lane, 0..255 leading virtual blocks, final blocks
-    of many lengths), TLS and explicit AD (0..255 bytes), 16-byte aligned
-    records and records at odd strides (byte-granular load/store paths), an odd
-    record count (an inactive slot in the last workgroup), and a tampered tag;
-    both kernel forms against the oracle byte for byte."""
+@pytest.mark.parametrize("adlen", [13, 0, 1, 7, 8, 24, 100, 255])
+def test_full_record_kernel_geometries(gpu, oracle, kernel_form, adlen):
+    """Full 16 KiB records (the wave-per-record kernel's batches) for TLS and
+    explicit AD of every stream phase (|ad| + 8 mod 16 = 5, 8, 9, 15, 0, 12,
+    12, 7: MAC chunks split 11/5, 8/8, ... between blocks; delta 0 and 1),
+    record counts that leave 1..7 inactive waves in the last workgroup, strides
+    with padding, per-record key_index and seq arrays, then open with a tampered
+    tag byte, a tampered ciphertext byte and a tampered AD; both kernel forms
+    against the oracle byte for byte."""
     torch = torch_mod()
     from suruga_amd import batch as B
 
-    keys = dev_bytes(KEY).view(1, 32)
-    for n in LS_LENGTHS:
-        for skew in (0, 3):
-            count = 5
-            rng = np.random.default_rng(n * 7 + skew + adlen)
-            si, so = n + skew, n + 16 + skew
-            pt_h = rng.bytes(si * count)
-            nonces_h = rng.bytes(8 * count)
-            ads_h = rng.bytes(max(adlen, 1) * count)
-            seq0 = 0xFFFFFFFE
+    n = 16384
+    rng = np.random.default_rng(77 + adlen)
+    keys_h = rng.bytes(4 * 32)
+    keys = dev_bytes(keys_h).view(4, 32)
+    for count, pad in ((1, 0), (5, 16), (8, 0), (9, 48), (23, 0)):
+        si, so = n + pad, n + 16 + pad
+        pt_h = rng.bytes(si * count)
+        nonces_h = rng.bytes(8 * count)
+        ads_h = rng.bytes(max(adlen, 1) * count)
+        kidx = (np.arange(count) * 3 % 4).astype(np.uint32)
+        seqs = (np.arange(count, dtype=np.uint64) * 0x100000001 + 0xFFFFFFF0)
+        dev = lambda a: torch.from_numpy(a.view(np.int64) if a.dtype == np.uint64 else a.view(np.int32)).to("cuda")
+        if adlen == 13:
+            mode = dict(seq=dev(seqs))
+        else:
+            mode = dict(tls=False, nonces=dev_bytes(nonces_h), ads=dev_bytes(ads_h), ad_len=adlen,
+                        ad_stride=max(adlen, 1))
+        mode["key_index"] = dev(kidx)
+        ct = torch.zeros(so * count, dtype=torch.uint8, device="cuda")
+        B.seal(B.Batch(count=count, keys=keys, inp=dev_bytes(pt_h), out=ct, uniform_len=n, in_stride=si,
+                       out_stride=so, **mode))
+        torch.cuda.synchronize()
+        ct_h = bytearray(host(ct))
+        for i in range(count):
+            k = keys_h[32 * kidx[i]:32 * kidx[i] + 32]
             if adlen == 13:
-                mode = dict(seq0=seq0)
+                s = int(seqs[i])
+                nonce, ad = struct.pack(">Q", s), oracle.tls_ad(s, n)
             else:
-                mode = dict(tls=False, nonces=dev_bytes(nonces_h), ads=dev_bytes(ads_h), ad_len=adlen,
-                            ad_stride=max(adlen, 1))
-            ct = torch.zeros(so * count, dtype=torch.uint8, device="cuda")
-            B.seal(B.Batch(count=count, keys=keys, inp=dev_bytes(pt_h), out=ct, uniform_len=n, in_stride=si,
-                           out_stride=so, **mode))
-            torch.cuda.synchronize()
-            ct_h = bytearray(host(ct))
-            for i in range(count):
-                if adlen == 13:
-                    nonce, ad = struct.pack(">Q", seq0 + i), oracle.tls_ad(seq0 + i, n)
-                else:
-                    nonce, ad = nonces_h[8 * i:8 * i + 8], ads_h[i * max(adlen, 1):i * max(adlen, 1) + adlen]
-                exp = oracle.seal(KEY, nonce, pt_h[i * si:i * si + n], ad)
-                assert bytes(ct_h[i * so:i * so + n + 16]) == exp, (kernel_form, adlen, n, skew, i)
-            ct_h[2 * so + n + 5] ^= 0x40  # record 2: tag byte
-            back = torch.zeros(si * count, dtype=torch.uint8, device="cuda")
-            st = torch.full((count,), 0xFF, dtype=torch.uint8, device="cuda")
-            B.open_(B.Batch(count=count, keys=keys, inp=dev_bytes(bytes(ct_h)), out=back, uniform_len=n + 16,
-                            in_stride=so, out_stride=si, status=st, **mode))
-            torch.cuda.synchronize()
-            assert host(st) == bytes([0, 0, 1, 0, 0]), (kernel_form, adlen, n, skew)
-            back_h = host(back)
-            for i in range(count):  # decrypted unconditionally (chacha20_poly1305.rs:80-82)
-                assert back_h[i * si:i * si + n] == pt_h[i * si:i * si + n], (kernel_form, adlen, n, skew, i)
+                nonce, ad = nonces_h[8 * i:8 * i + 8], ads_h[i * max(adlen, 1):i * max(adlen, 1) + adlen]
+            exp = oracle.seal(k, nonce, pt_h[i * si:i * si + n], ad)
+            assert bytes(ct_h[i * so:i * so + n + 16]) == exp, (kernel_form, adlen, count, i)
+        exp_st = bytearray(count)
+        ct_h[(count - 1) * so + n + 5] ^= 0x40  # last record: a tag byte
+        exp_st[count - 1] = 1
+        if count > 2:
+            ct_h[1 * so + 4097] ^= 0x01  # record 1: a ciphertext byte of chunk 1
+            exp_st[1] = 1
+        ads_in = bytearray(ads_h)
+        if count > 3 and adlen not in (0, 13):
+            ads_in[3 * max(adlen, 1)] ^= 0x10  # record 3: its AD (explicit mode)
+            exp_st[3] = 1
+        if adlen != 13:
+            mode["ads"] = dev_bytes(bytes(ads_in))
+        back = torch.zeros(si * count, dtype=torch.uint8, device="cuda")
+        st = torch.full((count,), 0xFF, dtype=torch.uint8, device="cuda")
+        B.open_(B.Batch(count=count, keys=keys, inp=dev_bytes(bytes(ct_h)), out=back, uniform_len=n + 16,
+                        in_stride=so, out_stride=si, status=st, **mode))
+        torch.cuda.synchronize()
+        assert host(st) == bytes(exp_st), (kernel_form, adlen, count)
+        back_h = host(back)
+        for i in range(count):  # decrypted unconditionally (chacha20_poly1305.rs:80-82)
+            exp_pt = bytearray(pt_h[i * si:i * si + n])
+            if i == 1 and count > 2:
+                exp_pt[4097] ^= 0x01
+            assert back_h[i * si:i * si + n] == bytes(exp_pt), (kernel_form, adlen, count, i)
+
+
+def test_full_record_kernel_persistent_groups(gpu, oracle, kernel_form):
+    """More record groups than resident workgroups (each workgroup walks several
+    groups and prefetches the next record's first chunk and keying table), with
+    a partial last group: 8195 x 16 KiB, compared byte for byte with the oracle
+    on a strided sample plus an XOR-fold of every tag, and opened on device."""
+    torch = torch_mod()
+    from suruga_amd import batch as B
+
+    count, n = 8195, 16384
+    pt, ct, back, st = tls_batch(count, n, seq0=0xFFFFFF00)
+    mism = torch.zeros(1, dtype=torch.int64, device="cuda")
+    B.compare_records(pt, n, back, n, n, count, mism)
+    torch.cuda.synchronize()
+    assert int(mism.item()) == 0 and host(st) == bytes(count)
+    pt_h = host(pt)
+    ct_ref = oracle.seal_batch_tls(KEY, 0xFFFFFF00, pt_h, n, count, threads=min(16, os.cpu_count() or 1))
+    ref = np.frombuffer(ct_ref, dtype=np.uint8).reshape(count, n + 16)
+    got = ct.view(count, n + 16)
+    tags = got[:, n:].cpu().numpy()
+    assert np.bitwise_xor.reduce(tags, axis=0).tobytes() == np.bitwise_xor.reduce(ref[:, n:], axis=0).tobytes()
+    assert np.array_equal(tags, ref[:, n:])
+    for i in list(range(0, count, 511)) + [count - 3, count - 2, count - 1]:
+        assert np.array_equal(got[i].cpu().numpy(), ref[i]), i
