@@ -314,9 +314,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const uint32_t wave = uniform(threadIdx.x >> 6), lane = threadIdx.x & 63u;
     uint8_t* buf = lds + wave * kWprWaveLds;
-    uint8_t* lines = buf + kWprLinesOff;  // also the landing area of the record's keying table
+    uint8_t* lines = buf + kWprLinesOff;
+    const uint8_t* table = buf + kWprChunk;  // chunk buffer 1 holds the keying table between records
     const uint32_t lds_wave = uniform((uint32_t)(uintptr_t)buf);
-    const uint32_t lds_lines = uniform(lds_wave + kWprLinesOff);
+    const uint32_t lds_table = uniform(lds_wave + kWprChunk);
     const uint32_t hh = lane >> 5, q = lane & 31u;
     const uint32_t adlen = TLS ? 13u : p.ad_len;
     const uint32_t sigma = (adlen + 8u) & 15u;
@@ -338,8 +339,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     auto dma_chunk_of = [&](uint32_t rec, uint32_t c) {
         dma_chunk(lds_wave + kWprChunk * (c & 1u), p.in + p.in_stride * rec + kWprChunk * c + 16u * wunit);
     };
-    auto dma_table_of = [&](uint32_t rec) {
-        if (lane < kWprRecWords / 4u) dma_one(lds_lines, p.ws + (uint64_t)rec * kWprRecWords + 4u * lane);
+    auto dma_table_of = [&](uint32_t rec) {  // into chunk buffer 1, free between records
+        if (lane < kWprRecWords / 4u) dma_one(lds_table, p.ws + (uint64_t)rec * kWprRecWords + 4u * lane);
     };
     uint32_t g = blockIdx.x;
     if (g < ngroups && g * kWprWaves + wave < p.count) {
@@ -378,13 +379,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
             rx[0] = cload(tg, 0); rx[1] = cload(tg, 1); rx[2] = cload(tg, 2); rx[3] = cload(tg, 3);
         }
 
-        // ---- the keying table has landed (it was followed by the previous
-        // record's four chunk stores and its tag / status store)
+        // ---- the keying table has landed (it was followed only by the previous
+        // record's tag / status store; the chunk-0 DMA is older)
         if (first) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
         first = false;
         wave_lds_sync();
-        const uint32_t* tab = reinterpret_cast<const uint32_t*>(lines);
+        const uint32_t* tab = reinterpret_cast<const uint32_t*>(table);
         // row weight W = 2^(32 hh) r^(4 (31 - q)) = hi[hh][a] lo[b], 31 - q = 8 a + b
         const uint32_t e = 31u - q;
         const F26 W = fmul(load_f26(tab + kWHi + 20u * hh + 5u * (e >> 3)), load_f26(tab + kWLo + 5u * (e & 7u)));
@@ -399,7 +400,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
             const uint32_t k = lane / 5u, u = lane - 5u * k;
             lv = fmul(load_f26(tab + kWRd + 5u * u), load_f26(tab + kWTk + 5u * k));
         }
-        wave_lds_sync();  // every table read is done before the lines overwrite it
         if (lane < kWprLines) {
             const F26 v = canonical(lv);
             uint32_t c;  // digits = the bytes of v + 0x80..80, each ^ 0x80
@@ -424,6 +424,33 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
 #pragma unroll
         for (int i = 0; i < 16; ++i) acc[i] = 1 << 24;
 
+        // MAC step (jj, i): T fragment = the V window of line iv = 5 k + 4 - i for
+        // bytes a' < 16 - sigma, else the P window of line iv - 1 (k = (1 - hh) +
+        // 2 (3 - jj)); B operand = chunk i of the lane's block, byte - 128.
+        auto mac_load = [&](uint32_t jj, uint32_t i, u32x4& V, u32x4& P) {
+            const uint32_t iv = 5u * ((1u - hh) + 2u * (3u - jj)) + 4u - i;
+            V = ldu16(lines + kWprLineBytes * iv + 47u - q);
+            P = ldu16(lines + kWprLineBytes * iv - 17u - q);
+        };
+        auto mac_mfma = [&](const u32x4& V, const u32x4& P, const u32x4& a) {
+            const u32x4 f = (V & vmask) | (P & ~vmask);
+            acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(__builtin_bit_cast(i32x4, f),
+                                                         __builtin_bit_cast(i32x4, a ^ 0x80808080u), acc, 0, 0, 0);
+        };
+        // The MAC of iteration j - 1 runs inside iteration j's rounds: its T
+        // windows are read one double round ahead of each MFMA and the MFMAs are
+        // two double rounds apart, so neither an LDS latency nor the MFMA chain
+        // ever stalls a wave at a lock-step barrier (sched_barrier pins the
+        // placement).  A holds the previous iteration's ciphertext chunks.
+        u32x4 A[4] = {};
+        u32x4 V0 = {}, P0 = {}, V1 = {}, P1 = {};
+#define SG_DR()                                                                                                   \
+    asm volatile(SG_CHACHA_DR_NB1_BAR1                                                                            \
+                 : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]), "+v"(x[7]), \
+                   "+v"(x[8]), "+v"(x[9]), "+v"(x[10]), "+v"(x[11]), "+v"(x[12]), "+v"(x[13]), "+v"(x[14]),         \
+                   "+v"(x[15]))
+#define SG_PIN() __builtin_amdgcn_sched_barrier(0)
+
 #pragma unroll
         for (uint32_t j = 0; j < 4u; ++j) {
             // chunk j has landed in buffer j & 1 (j >= 1: it was followed by the
@@ -431,9 +458,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
             if (j > 0u) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
             wave_lds_sync();
             uint8_t* cb = buf + kWprChunk * (j & 1u);
-            u32x4 D[4];
-#pragma unroll
-            for (uint32_t i = 0; i < 4u; ++i) D[i] = ld16(cb + 16u * (4u * lane + (i ^ xq)));
             // prefetch the next chunk into the other buffer (its last reader, the
             // read-out of chunk j - 1, has completed: its data was stored)
             if (j < 3u) {
@@ -446,38 +470,56 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
             const uint32_t ctr = 64u * j + lane + 1u;
             uint32_t x[16] = {kSigma0, kSigma1, kSigma2, kSigma3, kw[0], kw[1], kw[2], kw[3],
                               kw[4],   kw[5],   kw[6],   kw[7],   ctr,   0u,    n14,   n15};
-#pragma unroll 1
-            for (int r = 0; r < 10; ++r)
-                asm volatile(SG_CHACHA_DR_NB1_BAR1
-                             : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]),
-                               "+v"(x[7]), "+v"(x[8]), "+v"(x[9]), "+v"(x[10]), "+v"(x[11]), "+v"(x[12]), "+v"(x[13]),
-                               "+v"(x[14]), "+v"(x[15]));
-            // feed-forward (chacha20.rs:104-106), XOR (chacha20.rs:143-153), and the
-            // MAC step of each chunk on the ciphertext: received (open) or just
-            // produced (seal).  Step (j, i): T fragment = the V window of line
-            // iv = 5 k + 4 - i for bytes a' < 16 - sigma, else the P window of line iv - 1
-            const u32x4 ks[4] = {u32x4{x[0] + kSigma0, x[1] + kSigma1, x[2] + kSigma2, x[3] + kSigma3},
-                                 u32x4{x[4] + kw[0], x[5] + kw[1], x[6] + kw[2], x[7] + kw[3]},
-                                 u32x4{x[8] + kw[4], x[9] + kw[5], x[10] + kw[6], x[11] + kw[7]},
-                                 u32x4{x[12] + ctr, x[13], x[14] + n14, x[15] + n15}};
-            const uint32_t kk = (1u - hh) + 2u * (3u - j);
-            u32x4 O[4];
+            u32x4 D[4];
+            SG_PIN();
+            SG_DR();
+            SG_PIN();
+            if (j > 0u) mac_load(j - 1u, 0u, V0, P0);
+            SG_PIN();
+            SG_DR();
+            SG_PIN();
+            if (j > 0u) {
+                mac_mfma(V0, P0, A[0]);
+                mac_load(j - 1u, 1u, V1, P1);
+            }
+            SG_PIN();
+            SG_DR();
+            SG_PIN();
+            if (j > 0u) {
+                mac_mfma(V1, P1, A[1]);
+                mac_load(j - 1u, 2u, V0, P0);
+            }
+            SG_PIN();
+            SG_DR();
+            SG_PIN();
+            if (j > 0u) {
+                mac_mfma(V0, P0, A[2]);
+                mac_load(j - 1u, 3u, V1, P1);
+            }
+            SG_PIN();
+            SG_DR();
+            SG_PIN();
+            if (j > 0u) mac_mfma(V1, P1, A[3]);
+            SG_PIN();
+            SG_DR();
+            SG_DR();
+            SG_DR();
+            SG_DR();
+            SG_PIN();
 #pragma unroll
-            for (uint32_t i = 0; i < 4u; ++i) {
-                O[i] = D[i] ^ ks[i];
-                const uint32_t iv = 5u * kk + 4u - i;
-                const u32x4 V = ldu16(lines + kWprLineBytes * iv + 47u - q);
-                const u32x4 P = ldu16(lines + kWprLineBytes * iv - 17u - q);
-                const u32x4 f = (V & vmask) | (P & ~vmask);
-                acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(__builtin_bit_cast(i32x4, f),
-                                                             __builtin_bit_cast(i32x4, (OPEN ? D[i] : O[i]) ^ 0x80808080u),
-                                                             acc, 0, 0, 0);
-            }
-            if (j == 3u && next) {  // the lines are read: the next record's keying table may land
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                wave_lds_sync();
-                dma_table_of(nrec);
-            }
+            for (uint32_t i = 0; i < 4u; ++i) D[i] = ld16(cb + 16u * (4u * lane + (i ^ xq)));
+            SG_PIN();
+            SG_DR();
+            SG_PIN();
+            // feed-forward (chacha20.rs:104-106) and XOR (chacha20.rs:143-153)
+            u32x4 O[4];
+            O[0] = D[0] ^ u32x4{x[0] + kSigma0, x[1] + kSigma1, x[2] + kSigma2, x[3] + kSigma3};
+            O[1] = D[1] ^ u32x4{x[4] + kw[0], x[5] + kw[1], x[6] + kw[2], x[7] + kw[3]};
+            O[2] = D[2] ^ u32x4{x[8] + kw[4], x[9] + kw[5], x[10] + kw[6], x[11] + kw[7]};
+            O[3] = D[3] ^ u32x4{x[12] + ctr, x[13], x[14] + n14, x[15] + n15};
+            // the MAC reads the ciphertext: received (open) or just produced (seal)
+#pragma unroll
+            for (uint32_t i = 0; i < 4u; ++i) A[i] = OPEN ? D[i] : O[i];
 
             // the output leaves through the same slice, lane-contiguously
 #pragma unroll
@@ -494,6 +536,22 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
             }
             wave_lds_sync();
         }
+#undef SG_DR
+#undef SG_PIN
+        // buffer 1 (chunk 3's) is free: the next record's keying table lands there
+        if (next) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            dma_table_of(nrec);
+        }
+        // the MAC of iteration 3
+        mac_load(3u, 0u, V0, P0);
+        mac_load(3u, 1u, V1, P1);
+        mac_mfma(V0, P0, A[0]);
+        mac_load(3u, 2u, V0, P0);
+        mac_mfma(V1, P1, A[1]);
+        mac_load(3u, 3u, V1, P1);
+        mac_mfma(V0, P0, A[2]);
+        mac_mfma(V1, P1, A[3]);
 
         // ---- assemble X = sum_r D[c_r][q] 2^(8 c_r - 32 hh), c_r = (r & 3) + 8 (r >> 2) + 4 hh
         uint32_t xw[8];
