@@ -291,6 +291,32 @@ __device__ __forceinline__ F26 reduce_words8(const uint32_t w[8]) {
     return f;
 }
 
+// Phase timing (experiment builds only, -DSG_WPR_PROFILE=1; the output is
+// unchanged): each wave accumulates s_memtime deltas per phase in SGPRs and
+// writes them once at its end; tools/wpr_phase.py reads them back through
+// sg_wpr_profile_read.
+#ifndef SG_WPR_PROFILE
+#define SG_WPR_PROFILE 0
+#endif
+constexpr uint32_t kProfPhases = 8, kProfWaves = 4096;
+#if SG_WPR_PROFILE
+__device__ unsigned long long g_wpr_prof[kProfWaves][kProfPhases];
+#define SG_TICK(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#define SG_ACC(k, a, b) prof[k] += (b) - (a)
+#else
+#define SG_TICK(v)
+#define SG_ACC(k, a, b)
+#endif
+
+// A zero vector materialised where it is used (a hoisted constant would hold
+// four VGPRs across the whole record loop).
+__device__ __forceinline__ u32x4 zero4() {
+    u32x4 z;
+    asm volatile("v_mov_b32 %0, 0\nv_mov_b32 %1, 0\nv_mov_b32 %2, 0\nv_mov_b32 %3, 0"
+                 : "=v"(z[0]), "=v"(z[1]), "=v"(z[2]), "=v"(z[3]));
+    return z;
+}
+
 // Scalar loads of wave-uniform inputs (key table, key index, sequence numbers,
 // explicit nonces, the received tag): the constant address space makes hipcc
 // emit s_load (counted on lgkmcnt), so no compiler-counted vector load ever
@@ -314,10 +340,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const uint32_t wave = uniform(threadIdx.x >> 6), lane = threadIdx.x & 63u;
     uint8_t* buf = lds + wave * kWprWaveLds;
-    uint8_t* lines = buf + kWprLinesOff;
-    const uint8_t* table = buf + kWprChunk;  // chunk buffer 1 holds the keying table between records
+    uint8_t* lines = buf + kWprLinesOff;  // also the landing area of the record's keying table
     const uint32_t lds_wave = uniform((uint32_t)(uintptr_t)buf);
-    const uint32_t lds_table = uniform(lds_wave + kWprChunk);
+    const uint32_t lds_lines = uniform(lds_wave + kWprLinesOff);
     const uint32_t hh = lane >> 5, q = lane & 31u;
     const uint32_t adlen = TLS ? 13u : p.ad_len;
     const uint32_t sigma = (adlen + 8u) & 15u;
@@ -327,6 +352,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     // LDS swizzle: 16-byte unit 4 t + c of a chunk lives at 4 t + (c ^ ((t >> 2) & 3))
     const uint32_t wunit = (lane & ~3u) | ((lane ^ (lane >> 4)) & 3u);  // unit of global position 64 k + lane
     const uint32_t xq = (lane >> 2) & 3u;
+    // the lane's MAC window base (line 5 (1 - hh), dword of byte 47 - q) and shift
+    const uint8_t* mac_base = lines + 240u * (1u - hh) + 4u * ((47u - q) >> 2);
+    const uint32_t mac_shift = (47u - q) & 3u;
     const uint32_t ngroups = (p.count + kWprWaves - 1u) / kWprWaves;
 
     // Chunk c of a record is fetched by LDS-DMA into buffer c & 1, one chunk
@@ -339,8 +367,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     auto dma_chunk_of = [&](uint32_t rec, uint32_t c) {
         dma_chunk(lds_wave + kWprChunk * (c & 1u), p.in + p.in_stride * rec + kWprChunk * c + 16u * wunit);
     };
-    auto dma_table_of = [&](uint32_t rec) {  // into chunk buffer 1, free between records
-        if (lane < kWprRecWords / 4u) dma_one(lds_table, p.ws + (uint64_t)rec * kWprRecWords + 4u * lane);
+    auto dma_table_of = [&](uint32_t rec) {  // into the line area
+        if (lane < kWprRecWords / 4u) dma_one(lds_lines, p.ws + (uint64_t)rec * kWprRecWords + 4u * lane);
     };
     uint32_t g = blockIdx.x;
     if (g < ngroups && g * kWprWaves + wave < p.count) {
@@ -348,8 +376,22 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
         dma_table_of(g * kWprWaves + wave);
     }
     bool first = true;
+    // the previous chunk's output waits in its LDS buffer and leaves during
+    // the next chunk's first double rounds (pend: it belongs to an active record)
+    bool pend = false;
+    uint8_t* pend_dst = p.out;
 
+#if SG_WPR_PROFILE
+    uint64_t prof[kProfPhases] = {};
+    const uint64_t t_start = __builtin_amdgcn_s_memtime();
+    uint64_t t_prev = t_start;
+#endif
     for (; g < ngroups; g += gridDim.x) {
+        SG_TICK(t_rs);
+        SG_ACC(7, t_prev, t_rs);  // epilogue + loop overhead of the previous record
+#if SG_WPR_PROFILE
+        prof[6] += 1;  // records (groups) this wave ran
+#endif
         const uint32_t rec = g * kWprWaves + wave;
         const bool active = rec < p.count;  // an inactive wave still runs every round and barrier
         const uint32_t recl = rec < p.count ? rec : p.count - 1u;
@@ -385,7 +427,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
         else asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
         first = false;
         wave_lds_sync();
-        const uint32_t* tab = reinterpret_cast<const uint32_t*>(table);
+        SG_TICK(t_tw);
+        SG_ACC(0, t_rs, t_tw);  // wait for the keying table
+        const uint32_t* tab = reinterpret_cast<const uint32_t*>(lines);
         // row weight W = 2^(32 hh) r^(4 (31 - q)) = hi[hh][a] lo[b], 31 - q = 8 a + b
         const uint32_t e = 31u - q;
         const F26 W = fmul(load_f26(tab + kWHi + 20u * hh + 5u * (e >> 3)), load_f26(tab + kWLo + 5u * (e & 7u)));
@@ -400,6 +444,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
             const uint32_t k = lane / 5u, u = lane - 5u * k;
             lv = fmul(load_f26(tab + kWRd + 5u * u), load_f26(tab + kWTk + 5u * k));
         }
+        wave_lds_sync();  // every table read is done before the lines overwrite it
         if (lane < kWprLines) {
             const F26 v = canonical(lv);
             uint32_t c;  // digits = the bytes of v + 0x80..80, each ^ 0x80
@@ -410,15 +455,18 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
             d[3] = addc((v.v3 >> 18) | (v.v4 << 8), 0x80808080u, c, &c) ^ 0x80808080u;
             d[4] = ((v.v4 >> 24) + 0x80u + c) ^ 0x80u;
             uint8_t* ln = lines + kWprLineBytes * lane;
-            st16(ln, u32x4{0u, 0u, 0u, 0u});
-            st16(ln + 16, u32x4{0u, 0u, 0u, 0u});
-            st16(ln + 32, u32x4{0u, 0u, 0u, 0u});
+            const u32x4 z = zero4();
+            st16(ln, z);
+            st16(ln + 16, z);
+            st16(ln + 32, z);
 #pragma unroll
             for (uint32_t i = 0; i < 17u; ++i) ln[47u - sigma - i] = (uint8_t)(d[i >> 2] >> (8u * (i & 3u)));
         } else if (lane == kWprLines) {
-            st16(lines + kWprLines * kWprLineBytes, u32x4{0u, 0u, 0u, 0u});
+            st16(lines + kWprLines * kWprLineBytes, zero4());
         }
         wave_lds_sync();
+        SG_TICK(t_pl);
+        SG_ACC(1, t_tw, t_pl);  // W and the digit lines
 
         i32x16 acc;
 #pragma unroll
@@ -427,23 +475,66 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
         // MAC step (jj, i): T fragment = the V window of line iv = 5 k + 4 - i for
         // bytes a' < 16 - sigma, else the P window of line iv - 1 (k = (1 - hh) +
         // 2 (3 - jj)); B operand = chunk i of the lane's block, byte - 128.
-        auto mac_load = [&](uint32_t jj, uint32_t i, u32x4& V, u32x4& P) {
-            const uint32_t iv = 5u * ((1u - hh) + 2u * (3u - jj)) + 4u - i;
-            V = ldu16(lines + kWprLineBytes * iv + 47u - q);
-            P = ldu16(lines + kWprLineBytes * iv - 17u - q);
+        // The windows start at byte 47 - q of line iv and 31 - q of line iv - 1:
+        // both are read as aligned dwords (an unaligned 16-byte LDS read stalls
+        // the LDS pipe for the whole CU) and shifted into place with
+        // v_alignbyte by the lane's (47 - q) & 3.  TLS (sigma = 5) needs V words
+        // 0-2 and P words 2-3 only.
+        struct MacRaw {
+            uint32_t v[5], p[5];
         };
-        auto mac_mfma = [&](const u32x4& V, const u32x4& P, const u32x4& a) {
-            const u32x4 f = (V & vmask) | (P & ~vmask);
+        auto mac_load = [&](uint32_t jj, uint32_t i, MacRaw& R) {
+            const uint8_t* b = mac_base + 480u * (3u - jj) + 48u * (4u - i);
+            const uint32_t* vb = reinterpret_cast<const uint32_t*>(b);
+            const uint32_t* pb = reinterpret_cast<const uint32_t*>(b - 64);
+            if constexpr (TLS) {
+#pragma unroll
+                for (int t = 0; t < 4; ++t) R.v[t] = vb[t];
+#pragma unroll
+                for (int t = 2; t < 5; ++t) R.p[t] = pb[t];
+            } else {
+#pragma unroll
+                for (int t = 0; t < 5; ++t) {
+                    R.v[t] = vb[t];
+                    R.p[t] = pb[t];
+                }
+            }
+        };
+        auto mac_frag = [&](const MacRaw& R) -> u32x4 {
+            u32x4 f;
+            if constexpr (TLS) {  // bytes 0-10 from V, 11-15 from P
+                f[0] = __builtin_amdgcn_alignbyte(R.v[1], R.v[0], mac_shift);
+                f[1] = __builtin_amdgcn_alignbyte(R.v[2], R.v[1], mac_shift);
+                const uint32_t v2 = __builtin_amdgcn_alignbyte(R.v[3], R.v[2], mac_shift);
+                const uint32_t p2 = __builtin_amdgcn_alignbyte(R.p[3], R.p[2], mac_shift);
+                f[2] = (v2 & 0x00ffffffu) | (p2 & 0xff000000u);
+                f[3] = __builtin_amdgcn_alignbyte(R.p[4], R.p[3], mac_shift);
+            } else {
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const uint32_t vt = __builtin_amdgcn_alignbyte(R.v[t + 1], R.v[t], mac_shift);
+                    const uint32_t pt = __builtin_amdgcn_alignbyte(R.p[t + 1], R.p[t], mac_shift);
+                    f[t] = (vt & vmask[t]) | (pt & ~vmask[t]);
+                }
+            }
+            return f;
+        };
+        auto mac_mfma_f = [&](const u32x4& f, const u32x4& a) {
             acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(__builtin_bit_cast(i32x4, f),
                                                          __builtin_bit_cast(i32x4, a ^ 0x80808080u), acc, 0, 0, 0);
         };
+        auto mac_mfma = [&](const MacRaw& R, const u32x4& a) { mac_mfma_f(mac_frag(R), a); };
         // The MAC of iteration j - 1 runs inside iteration j's rounds: its T
         // windows are read one double round ahead of each MFMA and the MFMAs are
         // two double rounds apart, so neither an LDS latency nor the MFMA chain
         // ever stalls a wave at a lock-step barrier (sched_barrier pins the
-        // placement).  A holds the previous iteration's ciphertext chunks.
+        // placement).  A holds the previous iteration's ciphertext chunks.  The
+        // last iteration reads its own T fragments (F3) during its rounds, so the
+        // line area is free for the next record's keying table before this
+        // record's last stores are issued.
         u32x4 A[4] = {};
-        u32x4 V0 = {}, P0 = {}, V1 = {}, P1 = {};
+        MacRaw R0 = {}, R1 = {};
+        u32x4 F3[4] = {};
 #define SG_DR()                                                                                                   \
     asm volatile(SG_CHACHA_DR_NB1_BAR1                                                                            \
                  : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]), "+v"(x[7]), \
@@ -453,18 +544,15 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
 
 #pragma unroll
         for (uint32_t j = 0; j < 4u; ++j) {
-            // chunk j has landed in buffer j & 1 (j >= 1: it was followed by the
-            // four stores of chunk j - 1; j = 0: waited for with the table)
-            if (j > 0u) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            SG_TICK(t_js);
+            // chunk j has landed in buffer j & 1 (j >= 1: its DMA was the last
+            // memory operation of iteration j - 1; j = 0: waited for with the table)
+            if (j > 0u) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             wave_lds_sync();
+            SG_TICK(t_jw);
+            SG_ACC(2, t_js, t_jw);  // wait for the chunk
             uint8_t* cb = buf + kWprChunk * (j & 1u);
-            // prefetch the next chunk into the other buffer (its last reader, the
-            // read-out of chunk j - 1, has completed: its data was stored)
-            if (j < 3u) {
-                if (active) dma_chunk_of(rec, j + 1u);
-            } else if (next) {
-                dma_chunk_of(nrec, 0u);
-            }
+            uint8_t* pb = buf + kWprChunk * ((j + 1u) & 1u);  // the pending output
 
             // keystream block 64 j + lane + 1 (chacha20_poly1305.rs:52), lock-step rounds
             const uint32_t ctr = 64u * j + lane + 1u;
@@ -474,36 +562,80 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
             SG_PIN();
             SG_DR();
             SG_PIN();
-            if (j > 0u) mac_load(j - 1u, 0u, V0, P0);
+            if (j > 0u) mac_load(j - 1u, 0u, R0);
+            // the previous chunk's output leaves lane-contiguously, half a chunk
+            // per double round
+            u32x4 o0 = {}, o1 = {};
+            if (pend) {
+                o0 = ld16(pb + 16u * wunit);
+                o1 = ld16(pb + 1024u + 16u * wunit);
+            }
             SG_PIN();
             SG_DR();
             SG_PIN();
+            if (pend) {
+                st16(pend_dst + 16u * lane, o0);
+                st16(pend_dst + 1024u + 16u * lane, o1);
+                o0 = ld16(pb + 2048u + 16u * wunit);
+                o1 = ld16(pb + 3072u + 16u * wunit);
+            }
             if (j > 0u) {
-                mac_mfma(V0, P0, A[0]);
-                mac_load(j - 1u, 1u, V1, P1);
+                mac_mfma(R0, A[0]);
+                mac_load(j - 1u, 1u, R1);
+            }
+            SG_PIN();
+            SG_DR();
+            SG_PIN();
+            if (pend) {
+                st16(pend_dst + 2048u + 16u * lane, o0);
+                st16(pend_dst + 3072u + 16u * lane, o1);
+            }
+            // prefetch the next chunk into the buffer just read out (the stores
+            // consumed the read-out's data, so those LDS reads have completed)
+            if (j < 3u) {
+                if (active) dma_chunk_of(rec, j + 1u);
+            } else if (next) {
+                dma_chunk_of(nrec, 0u);
+            }
+            if (j > 0u) {
+                mac_mfma(R1, A[1]);
+                mac_load(j - 1u, 2u, R0);
             }
             SG_PIN();
             SG_DR();
             SG_PIN();
             if (j > 0u) {
-                mac_mfma(V1, P1, A[1]);
-                mac_load(j - 1u, 2u, V0, P0);
+                mac_mfma(R0, A[2]);
+                mac_load(j - 1u, 3u, R1);
             }
             SG_PIN();
             SG_DR();
             SG_PIN();
-            if (j > 0u) {
-                mac_mfma(V0, P0, A[2]);
-                mac_load(j - 1u, 3u, V1, P1);
+            if (j > 0u) mac_mfma(R1, A[3]);
+            SG_PIN();
+            SG_DR();
+            SG_PIN();
+            if (j == 3u) {
+                mac_load(3u, 0u, R0);
+                mac_load(3u, 1u, R1);
             }
             SG_PIN();
             SG_DR();
             SG_PIN();
-            if (j > 0u) mac_mfma(V1, P1, A[3]);
+            if (j == 3u) {
+                F3[0] = mac_frag(R0);
+                F3[1] = mac_frag(R1);
+                mac_load(3u, 2u, R0);
+                mac_load(3u, 3u, R1);
+            }
             SG_PIN();
             SG_DR();
-            SG_DR();
-            SG_DR();
+            SG_PIN();
+            if (j == 3u) {
+                F3[2] = mac_frag(R0);
+                F3[3] = mac_frag(R1);
+            }
+            SG_PIN();
             SG_DR();
             SG_PIN();
 #pragma unroll
@@ -511,6 +643,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
             SG_PIN();
             SG_DR();
             SG_PIN();
+            SG_TICK(t_jr);
+            SG_ACC(3, t_jw, t_jr);  // rounds (+ MAC of the previous chunk)
+            if (j == 3u && next) {  // the line area is read out: the next record's table lands there
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                dma_table_of(nrec);
+            }
             // feed-forward (chacha20.rs:104-106) and XOR (chacha20.rs:143-153)
             u32x4 O[4];
             O[0] = D[0] ^ u32x4{x[0] + kSigma0, x[1] + kSigma1, x[2] + kSigma2, x[3] + kSigma3};
@@ -520,38 +658,27 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
             // the MAC reads the ciphertext: received (open) or just produced (seal)
 #pragma unroll
             for (uint32_t i = 0; i < 4u; ++i) A[i] = OPEN ? D[i] : O[i];
+            if (j == 3u) {
+                SG_PIN();
+#pragma unroll
+                for (uint32_t i = 0; i < 4u; ++i) mac_mfma_f(F3[i], A[i]);
+                SG_PIN();
+            }
 
-            // the output leaves through the same slice, lane-contiguously
+            // the output waits in the same slice; it leaves during the next
+            // chunk's first double rounds
 #pragma unroll
             for (uint32_t i = 0; i < 4u; ++i) st16(cb + 16u * (4u * lane + (i ^ xq)), O[i]);
-            wave_lds_sync();
-            const u32x4 o0 = ld16(cb + 16u * wunit), o1 = ld16(cb + 1024u + 16u * wunit);
-            const u32x4 o2 = ld16(cb + 2048u + 16u * wunit), o3 = ld16(cb + 3072u + 16u * wunit);
-            if (active) {
-                uint8_t* dst = out + kWprChunk * j + 16u * lane;
-                st16(dst, o0);
-                st16(dst + 1024, o1);
-                st16(dst + 2048, o2);
-                st16(dst + 3072, o3);
-            }
-            wave_lds_sync();
+            pend = active;
+            pend_dst = out + kWprChunk * j;
+            SG_TICK(t_je);
+            SG_ACC(4, t_jr, t_je);  // feed-forward, XOR, staging, stores
+#if SG_WPR_PROFILE
+            t_prev = t_je;
+#endif
         }
 #undef SG_DR
 #undef SG_PIN
-        // buffer 1 (chunk 3's) is free: the next record's keying table lands there
-        if (next) {
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            dma_table_of(nrec);
-        }
-        // the MAC of iteration 3
-        mac_load(3u, 0u, V0, P0);
-        mac_load(3u, 1u, V1, P1);
-        mac_mfma(V0, P0, A[0]);
-        mac_load(3u, 2u, V0, P0);
-        mac_mfma(V1, P1, A[1]);
-        mac_load(3u, 3u, V1, P1);
-        mac_mfma(V0, P0, A[2]);
-        mac_mfma(V1, P1, A[3]);
 
         // ---- assemble X = sum_r D[c_r][q] 2^(8 c_r - 32 hh), c_r = (r & 3) + 8 (r >> 2) + 4 hh
         uint32_t xw[8];
@@ -591,11 +718,40 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
             }
         }
     }
+    if (pend) {  // the last record's last chunk
+        wave_lds_sync();
+        const uint8_t* pb = buf + kWprChunk;
+#pragma unroll
+        for (uint32_t k = 0; k < 4u; ++k) st16(pend_dst + 1024u * k + 16u * lane, ld16(pb + 1024u * k + 16u * wunit));
+    }
+#if SG_WPR_PROFILE
+    SG_TICK(t_end);
+    SG_ACC(7, t_prev, t_end);
+    prof[5] = t_end - t_start;  // the wave's whole life
+    const uint32_t wid = blockIdx.x * kWprWaves + wave;
+    if (lane == 0u && wid < kProfWaves) {
+#pragma unroll
+        for (uint32_t k = 0; k < kProfPhases; ++k) g_wpr_prof[wid][k] = prof[k];
+    }
+#endif
 }
 
 int g_cus[64];  // CUs per device ordinal (0: not read yet)
 
 }  // namespace
+
+#if SG_WPR_PROFILE
+}  // namespace sg
+extern "C" int sg_wpr_profile_read(unsigned long long* host, size_t n) {
+    const size_t bytes = sizeof(sg::g_wpr_prof);
+    if (n * sizeof(unsigned long long) < bytes) return -1;
+    if (hipMemcpyFromSymbol(host, HIP_SYMBOL(sg::g_wpr_prof), bytes) != hipSuccess) return -2;
+    static unsigned long long zero[sg::kProfWaves][sg::kProfPhases];
+    if (hipMemcpyToSymbol(HIP_SYMBOL(sg::g_wpr_prof), zero, bytes) != hipSuccess) return -3;
+    return (int)(bytes / sizeof(unsigned long long));
+}
+namespace sg {
+#endif
 
 hipError_t launch_wpr(const KParams& p, bool open, hipStream_t s, hipEvent_t ev_keyed, hipEvent_t ev_start) {
     const uint32_t kgrid = (p.count + kWprKeyThreads - 1u) / kWprKeyThreads;
