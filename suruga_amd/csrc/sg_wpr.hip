@@ -308,6 +308,13 @@ __device__ unsigned long long g_wpr_prof[kProfWaves][kProfPhases];
 #define SG_ACC(k, a, b)
 #endif
 
+// The double-round body (experiment builds may pick another barrier spacing
+// from tools/chacha_grp.inc; every form computes the same rounds)
+#ifndef SG_WPR_DR_ASM
+#define SG_WPR_DR_ASM SG_CHACHA_DR_NB1_BAR1
+#define SG_WPR_DR1_ASM SG_CHACHA_DR1_NB1_BAR1
+#endif
+
 // A zero vector materialised where it is used (a hoisted constant would hold
 // four VGPRs across the whole record loop).
 __device__ __forceinline__ u32x4 zero4() {
@@ -415,6 +422,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
             n14 = cload(p.nonces, 2ull * recl);
             n15 = cload(p.nonces, 2ull * recl + 1u);
         }
+        // The column quarter rounds 1-3 of the first double round see no block
+        // counter (word 13 is 0, chacha20.rs:114-121): the same for every lane
+        // and chunk of the record, so they run once per record on the SALU.
+        uint32_t u[16] = {kSigma0, kSigma1, kSigma2, kSigma3, kw[0], kw[1], kw[2], kw[3],
+                          kw[4],   kw[5],   kw[6],   kw[7],   0u,    0u,    n14,   n15};
+        SG_QR(u[1], u[5], u[9], u[13]) SG_QR(u[2], u[6], u[10], u[14]) SG_QR(u[3], u[7], u[11], u[15])
         uint32_t rx[4] = {0u, 0u, 0u, 0u};
         if constexpr (OPEN) {  // the received tag (chacha20_poly1305.rs:72-73)
             const uint8_t* tg = p.in + p.in_stride * recl + kWprN;
@@ -536,7 +549,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
         MacRaw R0 = {}, R1 = {};
         u32x4 F3[4] = {};
 #define SG_DR()                                                                                                   \
-    asm volatile(SG_CHACHA_DR_NB1_BAR1                                                                            \
+    asm volatile(SG_WPR_DR_ASM                                                                                    \
+                 : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]), "+v"(x[7]), \
+                   "+v"(x[8]), "+v"(x[9]), "+v"(x[10]), "+v"(x[11]), "+v"(x[12]), "+v"(x[13]), "+v"(x[14]),         \
+                   "+v"(x[15]))
+#define SG_DR1()                                                                                                  \
+    asm volatile(SG_WPR_DR1_ASM                                                                                   \
                  : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]), "+v"(x[7]), \
                    "+v"(x[8]), "+v"(x[9]), "+v"(x[10]), "+v"(x[11]), "+v"(x[12]), "+v"(x[13]), "+v"(x[14]),         \
                    "+v"(x[15]))
@@ -556,11 +574,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
 
             // keystream block 64 j + lane + 1 (chacha20_poly1305.rs:52), lock-step rounds
             const uint32_t ctr = 64u * j + lane + 1u;
-            uint32_t x[16] = {kSigma0, kSigma1, kSigma2, kSigma3, kw[0], kw[1], kw[2], kw[3],
-                              kw[4],   kw[5],   kw[6],   kw[7],   ctr,   0u,    n14,   n15};
+            uint32_t x[16] = {kSigma0, u[1], u[2], u[3], kw[0], u[5], u[6],  u[7],
+                              kw[4],   u[9], u[10], u[11], ctr,  u[13], u[14], u[15]};
             u32x4 D[4];
             SG_PIN();
-            SG_DR();
+            SG_DR1();
             SG_PIN();
             if (j > 0u) mac_load(j - 1u, 0u, R0);
             // the previous chunk's output leaves lane-contiguously, half a chunk
@@ -678,6 +696,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
 #endif
         }
 #undef SG_DR
+#undef SG_DR1
 #undef SG_PIN
 
         // ---- assemble X = sum_r D[c_r][q] 2^(8 c_r - 32 hh), c_r = (r & 3) + 8 (r >> 2) + 4 hh
