@@ -79,6 +79,30 @@ def test_batch_argument_errors_without_gpu(lib):
     assert lib.sg_seal_batch(C.byref(b)) == 0  # empty batch is a no-op
 
 
+def test_explicit_mode_limits_are_sg_e_arg_without_gpu(lib):
+    """explicit-mode AD above SG_MAX_AD_LEN (255) and records
+    above SG_MAX_RECORD_LEN (32 KiB) are SG_E_ARG, where the reference's
+    Encryptor::encrypt (cipher/mod.rs:22-24) accepts any length.  The checks
+    run before any device work, so they are pinned here on the CPU."""
+    from suruga_amd._native import SG_E_ARG, SgBatch
+
+    b = SgBatch()
+    b.count, b.num_keys, b.flags = 4, 1, 0  # explicit mode
+    b.keys, b.in_, b.out, b.nonces, b.ads = 0x1000, 0x2000, 0x3000, 0x4000, 0x5000
+    b.uniform_len, b.in_stride, b.out_stride = 64, 64, 80
+    b.ad_len = 256
+    assert lib.sg_seal_batch(C.byref(b)) == SG_E_ARG
+    assert b"SG_MAX_AD_LEN" in lib.sg_last_error()
+    b.ad_len = 255
+    b.uniform_len, b.in_stride, b.out_stride = 32769, 32769, 32785
+    assert lib.sg_seal_batch(C.byref(b)) == SG_E_ARG
+    assert b"SG_MAX_RECORD_LEN" in lib.sg_last_error()
+    b.status = 0x6000
+    b.uniform_len = 32769 + 16  # open: the ciphertext carries the tag
+    assert lib.sg_open_batch(C.byref(b)) == SG_E_ARG
+    assert b"SG_MAX_RECORD_LEN" in lib.sg_last_error()
+
+
 def test_single_record_argument_errors_without_gpu(lib):
     from suruga_amd._native import SG_E_ARG
 

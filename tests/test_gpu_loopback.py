@@ -1,0 +1,53 @@
+"""C4 on the GPU: an application stream through sg_write_records, a loopback
+TCP connection and sg_read_records (tools/tls_loopback.py, the TlsWriter /
+TlsReader data path of tls.rs:126-147 and :238-281 with the handshake
+bypassed as in src/test.rs:29-39).  Every wire byte the writer sent is
+compared with the oracle's TLS sealing of the same records (header, ct, tag:
+chacha20_poly1305.rs:48-59, tls.rs:103-112), and every byte the reader
+delivered with the stream that went in.  Also the copy-inclusive record path
+per direction (tools/record_path_bench.py) at a reduced size.
+"""
+from __future__ import annotations
+
+import struct
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT / "tools"))
+
+KEY_C2S = bytes(range(32))
+REC = 1 << 14
+
+
+def test_loopback_64mib_wire_equals_oracle(gpu, oracle):
+    import tls_loopback as TL
+
+    total, wchunk = 64 << 20, 16 << 20
+    res = TL.run(total, wchunk, 0, capture=True)
+    assert res["correct"], {k: v for k, v in res.items() if k != "wire"}
+    assert res["reader"]["bytes"] == total and res["reader"]["mismatched_bytes"] == 0
+    wire = res["wire"]
+    nrec = total // REC
+    assert res["writer"]["records"] == nrec and len(wire) == nrec * (5 + REC + 16)
+    stream = np.tile(TL.stream_pattern(wchunk), total // wchunk)
+    expect = oracle.seal_batch_tls(KEY_C2S, 0, stream.tobytes(), REC, nrec, threads=16)
+    w = np.frombuffer(wire, dtype=np.uint8).reshape(nrec, 5 + REC + 16)
+    hdr = bytes([23, 3, 3]) + struct.pack(">H", REC + 16)
+    assert (w[:, :5] == np.frombuffer(hdr, dtype=np.uint8)).all()
+    body = np.frombuffer(expect, dtype=np.uint8).reshape(nrec, REC + 16)
+    bad = np.nonzero((w[:, 5:] != body).any(axis=1))[0]
+    assert bad.size == 0, f"{bad.size} records differ from the oracle, first {bad[:8]}"
+
+
+def test_record_path_both_directions_bit_exact(gpu):
+    import record_path_bench as RP
+
+    r = RP.one(32 << 20, 8 << 20, 0)
+    assert r["correct"], r
+    assert r["records"] == (32 << 20) // REC

@@ -522,3 +522,26 @@ def test_full_record_kernel_persistent_groups(gpu, oracle, kernel_form):
     assert np.array_equal(tags, ref[:, n:])
     for i in list(range(0, count, 511)) + [count - 3, count - 2, count - 1]:
         assert np.array_equal(got[i].cpu().numpy(), ref[i]), i
+
+
+def test_single_record_limits(gpu, oracle):
+    """AD of 255 bytes and a 32768-byte record are accepted
+    and bit-exact; 256 bytes of AD and 32769-byte records are SG_E_ARG."""
+    import ctypes as C
+
+    from suruga_amd import ChaCha20Poly1305
+    from suruga_amd import _native as N
+
+    lib = N.load()
+    aead = ChaCha20Poly1305()
+    enc, dec = aead.new_encryptor(KEY), aead.new_decryptor(KEY)
+    nonce = bytes(range(8))
+    ad, pt = bytes(range(255)), oracle.fill_record(SEED, 3, 32768)
+    ct = enc.encrypt(nonce, pt, ad)
+    assert ct == oracle.seal(KEY, nonce, pt, ad)
+    assert dec.decrypt(nonce, ct, ad) == pt
+    out = (C.c_uint8 * (32769 + 16))()
+    assert lib.sg_seal(enc._ptr, nonce, 8, pt, 100, bytes(256), 256, out) == N.SG_E_ARG
+    big = bytes(32769)
+    assert lib.sg_seal(enc._ptr, nonce, 8, big, len(big), ad, 13, out) == N.SG_E_ARG
+    assert lib.sg_open(dec._ptr, nonce, 8, big + bytes(16), len(big) + 16, ad, 13, out) == N.SG_E_ARG

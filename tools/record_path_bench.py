@@ -1,0 +1,138 @@
+#!/usr/bin/env python3
+"""Copy-inclusive rate of the GPU record path, one direction at a time (C4's
+host side, tls.rs:126-130 write / :238-281 read).
+
+Writer: sg_write_records over a host buffer of application data (fragment into
+2^14-byte records, pinned staging, H2D, seal, D2H, 5-byte headers) into a host
+wire buffer.  Reader: sg_read_records over that wire back into a host buffer.
+Both are timed wall-clock around the calls, from and to pageable host memory,
+so every copy is inside the number.  The read-back is compared with the input
+byte for byte.  Prints one JSON line (and writes it with --json-out): GiB/s of
+application data per direction plus the per-GiB split of H2D, kernel, D2H and
+host framing time (sg_record_timing) for SG_COPY_THREADS = each --threads value.
+
+    python tools/record_path_bench.py [--bytes 1073741824] [--call-bytes 67108864]
+        [--threads 1,4,8] [--json-out profiles/r02_record_path.json]
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import subprocess
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+
+KEY = bytes(range(32))
+
+
+def one(total: int, call: int, device: int) -> dict:
+    import numpy as np
+
+    from suruga_amd import ChaCha20Poly1305
+    from suruga_amd import _native as N
+
+    lib = N.load()
+    data = np.random.default_rng(0xC4).integers(0, 256, size=total, dtype=np.uint8)
+    wire = np.empty(lib.sg_wire_bound(total), dtype=np.uint8)
+    back = np.empty(total, dtype=np.uint8)
+    aead = ChaCha20Poly1305(device)
+    enc, dec = aead.new_encryptor(KEY), aead.new_decryptor(KEY)
+
+    def timing(acc):
+        v = [C.c_double() for _ in range(4)]
+        lib.sg_record_timing(*[C.byref(x) for x in v])
+        for k, x in zip(("h2d", "kernel", "d2h", "host"), v):
+            acc[k] = acc.get(k, 0.0) + x.value
+
+    def write_all(acc):
+        wl = C.c_size_t(0)
+        seq, pos, wpos = 0, 0, 0
+        while pos < total:
+            n = min(call, total - pos)
+            seq += N.check(lib.sg_write_records(enc._ptr, seq, 23, 3, 3, C.c_void_p(data.ctypes.data + pos), n,
+                                                C.c_void_p(wire.ctypes.data + wpos), wire.size - wpos,
+                                                C.byref(wl)))
+            if acc is not None:
+                timing(acc)
+            pos += n
+            wpos += wl.value
+        return seq, wpos
+
+    def read_all(wlen, acc):
+        res = N.SgReadResult()
+        seq, pos, opos = 0, 0, 0
+        while pos < wlen:
+            n = min(call + (call >> 10) + 64, wlen - pos)  # about `call` bytes of records per call
+            N.check(lib.sg_read_records(dec._ptr, seq, C.c_void_p(wire.ctypes.data + pos), n,
+                                        C.c_void_p(back.ctypes.data + opos), back.size - opos, None, None,
+                                        1 << 20, C.byref(res)))
+            if res.error != N.SG_OK:
+                raise RuntimeError(f"record error {res.error} after {seq + res.records} records")
+            if acc is not None:
+                timing(acc)
+            seq += res.records
+            pos += res.consumed
+            opos += res.out_len
+        return seq, opos
+
+    write_all(None)  # warm-up: staging allocation, page faults of the buffers
+    wacc, racc = {}, {}
+    t0 = time.perf_counter()
+    nrec, wlen = write_all(wacc)
+    tw = time.perf_counter() - t0
+    read_all(wlen, None)
+    t0 = time.perf_counter()
+    rrec, olen = read_all(wlen, racc)
+    tr = time.perf_counter() - t0
+    ok = rrec == nrec and olen == total and bool(np.array_equal(back, data))
+    gib = total / 2**30
+    per = lambda acc: {k + "_ms_per_gib": round(v / gib, 2) for k, v in acc.items()}  # noqa: E731
+    return {"write_gibs": round(gib / tw, 3), "read_gibs": round(gib / tr, 3), "write_ms": round(tw * 1e3, 1),
+            "read_ms": round(tr * 1e3, 1), "records": nrec, "correct": ok, "write_split": per(wacc),
+            "read_split": per(racc)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--bytes", type=int, default=1 << 30)
+    ap.add_argument("--call-bytes", type=int, default=64 << 20, help="application bytes per write call")
+    ap.add_argument("--threads", default="1,4,8", help="SG_COPY_THREADS values (one child process each)")
+    ap.add_argument("--device", type=int, default=0)
+    ap.add_argument("--json-out")
+    ap.add_argument("--child", action="store_true")
+    ap.add_argument("--watchdog", type=float, default=0, help="dump every thread's stack and exit after this many s")
+    a = ap.parse_args()
+    if a.watchdog:
+        import faulthandler
+
+        faulthandler.dump_traceback_later(a.watchdog, exit=True)
+    if a.child:
+        print(json.dumps(one(a.bytes, a.call_bytes, a.device)))
+        return
+    runs = {}
+    for t in [int(x) for x in a.threads.split(",")]:
+        env = dict(os.environ, SG_COPY_THREADS=str(t))
+        p = subprocess.run([sys.executable, __file__, "--child", "--bytes", str(a.bytes), "--call-bytes",
+                            str(a.call_bytes), "--device", str(a.device)], env=env, capture_output=True, text=True,
+                           timeout=600)
+        if p.returncode != 0:
+            raise SystemExit(f"threads={t} failed:\n{p.stdout}\n{p.stderr}")
+        runs[str(t)] = json.loads(p.stdout.strip().splitlines()[-1])
+    out = {"config": f"C4 host side: {a.bytes} B application data, {a.call_bytes} B per sg_write_records call, "
+                     "pageable host buffers, one direction at a time, wall clock around the calls",
+           "host_cpus": len(os.sched_getaffinity(0)), "by_copy_threads": runs,
+           "correct": all(r["correct"] for r in runs.values())}
+    print(json.dumps(out))
+    if a.json_out:
+        Path(a.json_out).write_text(json.dumps(out, indent=1) + "\n")
+    sys.exit(0 if out["correct"] else 1)
+
+
+if __name__ == "__main__":
+    main()

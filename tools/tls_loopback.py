@@ -9,8 +9,11 @@ sg_read_records (parse headers, open on the GPU, strip framing).  Keys are
 fixed (the handshake is bypassed, as in src/test.rs:29-39's null_tls); every
 received byte is compared with what was sent.
 
-Prints one JSON line: end-to-end GiB/s of application data plus the time each
-side spent in H2D copies, kernels, D2H copies, host framing and socket I/O.
+Prints one JSON line (--json-out also writes it to a file): end-to-end GiB/s
+of application data plus the time each side spent in H2D copies, kernels, D2H
+copies, host framing and socket I/O, also per GiB.  ``run()`` is the same
+stream as a function; tests/test_gpu_loopback.py calls it with
+``capture=True`` and checks the captured wire against the oracle.
 """
 from __future__ import annotations
 
@@ -34,15 +37,17 @@ from suruga_amd import _native as N  # noqa: E402
 KEY_C2S = bytes(range(32))
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--bytes", type=int, default=1 << 30, help="application bytes (C4: 1 GiB)")
-    ap.add_argument("--write-chunk", type=int, default=16 << 20, help="bytes per write_application_data call")
-    ap.add_argument("--device", type=int, default=0)
-    args = ap.parse_args()
+def stream_pattern(wchunk: int):
+    """The application stream is this pattern repeated every wchunk bytes."""
+    return np.random.default_rng(0xC4).integers(0, 256, size=wchunk, dtype=np.uint8)
+
+
+def run(total: int = 1 << 30, wchunk: int = 16 << 20, device: int = 0, capture: bool = False) -> dict:
+    """One loopback stream; returns the JSON-able result (plus "wire": the
+    bytes the writer sent, when capture)."""
     lib = N.load()
-    total, wchunk = args.bytes, args.write_chunk
-    pattern = np.random.default_rng(0xC4).integers(0, 256, size=wchunk, dtype=np.uint8)
+    pattern = stream_pattern(wchunk)
+    captured = bytearray() if capture else None
 
     srv = socket.create_server(("127.0.0.1", 0))
     port = srv.getsockname()[1]
@@ -61,7 +66,7 @@ def main():
         import queue
 
         try:
-            enc = ChaCha20Poly1305(args.device).new_encryptor(KEY_C2S)
+            enc = ChaCha20Poly1305(device).new_encryptor(KEY_C2S)
             sock = socket.create_connection(("127.0.0.1", port))
             sock.setsockopt(socket.SOL_SOCKET, socket.SO_SNDBUF, 8 << 20)
             nbuf = 3
@@ -81,6 +86,8 @@ def main():
                     t0 = time.perf_counter()
                     sock.sendall(memoryview(wires[w])[:ln])
                     t_sock[0] += time.perf_counter() - t0
+                    if captured is not None:
+                        captured.extend(memoryview(wires[w])[:ln])
                     free.put(w)
 
             th = threading.Thread(target=sender)
@@ -100,6 +107,7 @@ def main():
             full.put(None)
             th.join()
             sock.shutdown(socket.SHUT_WR)
+            sock.close()
             d["socket_ms"] = t_sock[0] * 1e3
             d["records"] = seq
         except Exception as e:  # pragma: no cover - reported below
@@ -111,7 +119,7 @@ def main():
         import queue
 
         try:
-            dec = ChaCha20Poly1305(args.device).new_decryptor(KEY_C2S)
+            dec = ChaCha20Poly1305(device).new_decryptor(KEY_C2S)
             conn, _ = srv.accept()
             conn.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 8 << 20)
             blk = 8 << 20
@@ -173,6 +181,7 @@ def main():
                 buf[:have - c] = buf[c:have]
                 have -= c
             th.join()
+            conn.close()
             if have:
                 raise RuntimeError(f"{have} trailing bytes")
             d.update(socket_ms=t_sock[0] * 1e3, verify_ms=t_verify * 1e3, records=seq, bytes=got,
@@ -187,16 +196,43 @@ def main():
     tw.join()
     tr.join()
     wall = time.perf_counter() - t0
+    srv.close()
     ok = not errors and stats["reader"].get("bytes") == total and stats["reader"].get("mismatched_bytes") == 0
-    print(json.dumps({
+    gib = total / 2**30
+    per_gib = {side: {k.replace("_ms", "_ms_per_gib"): round(v / gib, 2) for k, v in stats[side].items()
+                      if k.endswith("_ms")} for side in ("writer", "reader")}
+    out = {
         "config": f"C4: {total} B application stream, TlsWriter/TlsReader batched GPU record layer over "
                   "loopback TCP, fixed keys (handshake bypassed)",
         "gib_per_s": round(total / wall / 2**30, 3), "wall_s": round(wall, 3), "correct": ok,
         "writer": {k: round(v, 1) if isinstance(v, float) else v for k, v in stats["writer"].items()},
         "reader": {k: round(v, 1) if isinstance(v, float) else v for k, v in stats["reader"].items()},
+        "per_gib": per_gib,
         "errors": errors,
-    }))
-    sys.exit(0 if ok else 1)
+    }
+    if capture:
+        out["wire"] = bytes(captured)
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--bytes", type=int, default=1 << 30, help="application bytes (C4: 1 GiB)")
+    ap.add_argument("--write-chunk", type=int, default=16 << 20, help="bytes per write_application_data call")
+    ap.add_argument("--device", type=int, default=0)
+    ap.add_argument("--json-out")
+    ap.add_argument("--watchdog", type=float, default=0, help="dump every thread's stack and exit after this many s")
+    args = ap.parse_args()
+    if args.watchdog:
+        import faulthandler
+
+        faulthandler.dump_traceback_later(args.watchdog, exit=True)
+    out = run(args.bytes, args.write_chunk, args.device)
+    line = json.dumps(out)
+    print(line)
+    if args.json_out:
+        Path(args.json_out).write_text(json.dumps(out, indent=1) + "\n")
+    sys.exit(0 if out["correct"] else 1)
 
 
 if __name__ == "__main__":
