@@ -334,6 +334,17 @@ __device__ __forceinline__ uint32_t cload(const void* base, uint64_t word) {
 }
 
 // One 16-byte LDS-DMA per lane: LDS [l0 + 16 lane, +16) <- g (lanes with exec set).
+// The same with a wave-uniform base address in SGPRs and the lane's 32-bit
+// offset in a VGPR (global_load_lds_dwordx4 saddr form): one VGPR per lane for
+// every DMA of the kernel instead of a 64-bit address per instruction.
+__device__ __forceinline__ void dma_sv(uint32_t l0, const void* sbase, uint32_t voff) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(voff), "s"(sbase), "s"(l0)
+                 : "memory");
+}
+
 __device__ __forceinline__ void dma_one(uint32_t l0, const void* g) {
     uint32_t keep;
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
@@ -580,45 +591,48 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
             SG_PIN();
             SG_DR1();
             SG_PIN();
+            // The previous chunk's output leaves lane-contiguously one 1 KiB piece
+            // per double round (read from LDS one gap ahead of its store), and
+            // piece k of the next chunk's DMA follows the store of output piece k
+            // (the same LDS range): the stores and DMAs of the 16 waves of a CU
+            // spread over five gaps instead of queueing behind each other.
+            auto out_piece = [&](uint32_t k) { return ld16(pb + 1024u * k + 16u * wunit); };
+            auto store_piece = [&](uint32_t k, const u32x4& v) { st16(pend_dst + 1024u * k + 16u * lane, v); };
+            auto dma_piece = [&](uint32_t k) {
+                if (j < 3u) {
+                    if (active)
+                        dma_sv(uniform(lds_wave + kWprChunk * ((j + 1u) & 1u) + 1024u * k),
+                               p.in + p.in_stride * rec + kWprChunk * (j + 1u) + 1024u * k, 16u * wunit);
+                } else if (next) {
+                    dma_sv(uniform(lds_wave + 1024u * k), p.in + p.in_stride * nrec + 1024u * k, 16u * wunit);
+                }
+            };
+            u32x4 oa = {}, ob = {};
             if (j > 0u) mac_load(j - 1u, 0u, R0);
-            // the previous chunk's output leaves lane-contiguously, half a chunk
-            // per double round
-            u32x4 o0 = {}, o1 = {};
-            if (pend) {
-                o0 = ld16(pb + 16u * wunit);
-                o1 = ld16(pb + 1024u + 16u * wunit);
-            }
+            if (pend) oa = out_piece(0u);
             SG_PIN();
             SG_DR();
             SG_PIN();
-            if (pend) {
-                st16(pend_dst + 16u * lane, o0);
-                st16(pend_dst + 1024u + 16u * lane, o1);
-                o0 = ld16(pb + 2048u + 16u * wunit);
-                o1 = ld16(pb + 3072u + 16u * wunit);
-            }
             if (j > 0u) {
                 mac_mfma(R0, A[0]);
                 mac_load(j - 1u, 1u, R1);
             }
+            if (pend) {
+                store_piece(0u, oa);
+                ob = out_piece(1u);
+            }
             SG_PIN();
             SG_DR();
             SG_PIN();
-            if (pend) {
-                st16(pend_dst + 2048u + 16u * lane, o0);
-                st16(pend_dst + 3072u + 16u * lane, o1);
-            }
-            // prefetch the next chunk into the buffer just read out (the stores
-            // consumed the read-out's data, so those LDS reads have completed)
-            if (j < 3u) {
-                if (active) dma_chunk_of(rec, j + 1u);
-            } else if (next) {
-                dma_chunk_of(nrec, 0u);
-            }
             if (j > 0u) {
                 mac_mfma(R1, A[1]);
                 mac_load(j - 1u, 2u, R0);
             }
+            if (pend) {
+                store_piece(1u, ob);
+                oa = out_piece(2u);
+            }
+            dma_piece(0u);
             SG_PIN();
             SG_DR();
             SG_PIN();
@@ -626,13 +640,21 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
                 mac_mfma(R0, A[2]);
                 mac_load(j - 1u, 3u, R1);
             }
+            if (pend) {
+                store_piece(2u, oa);
+                ob = out_piece(3u);
+            }
+            dma_piece(1u);
             SG_PIN();
             SG_DR();
             SG_PIN();
             if (j > 0u) mac_mfma(R1, A[3]);
+            if (pend) store_piece(3u, ob);
+            dma_piece(2u);
             SG_PIN();
             SG_DR();
             SG_PIN();
+            dma_piece(3u);
             if (j == 3u) {
                 mac_load(3u, 0u, R0);
                 mac_load(3u, 1u, R1);
