@@ -8,17 +8,21 @@
 namespace sg {
 
 constexpr uint32_t kThreads = 256;        // one record per 256-thread workgroup
-constexpr uint32_t kKeyRecWords = 104;    // per-record keying output (u32 words, 416 B)
+constexpr uint32_t kKeyRecWords = 88;     // per-record keying output (u32 words, 352 B)
 // keying record layout (u32 words): r[4] clamped Poly1305 r (radix 2^32),
 // s[4] (second half of keystream block 0), then with R = r^k (k = MAC blocks
-// per lane, see mac_geom in sg_kernels.hip), in radix 2^26:
-//   lo[8][5] = R^j       j = 0..7
-//   hi[8][5] = R^(8 i)   i = 0..7
-// so that MAC lane t = 8a + b scales its partial sum by R^(63-t) = hi[7-a] lo[7-b];
+// per lane, see mac_geom in sg_kernels.hip) 5-limb radix-2^26 powers ordered so
+// that a record with PL MAC lanes needs only a prefix (kKeyUsedWords(PL)):
+//   R^0 (as hi[0]), lo[j] = R^j (j = 0..7), hi[i] = R^(8 i) (i = 1..7)
+// MAC lane t scales its partial sum by R^(PL-1-t) = hi[e >> 3] lo[e & 7].
 constexpr uint32_t kR32Off = 0;
 constexpr uint32_t kSOff = 4;
-constexpr uint32_t kPowLoOff = 8;
-constexpr uint32_t kPowHiOff = 48;
+__host__ __device__ constexpr uint32_t key_lo_off(uint32_t j) { return 13u + 5u * j; }
+__host__ __device__ constexpr uint32_t key_hi_off(uint32_t i) { return i == 0u ? 8u : 48u + 5u * i; }
+__host__ __device__ constexpr uint32_t key_used_words(uint32_t PL) {
+    return PL <= 8u ? 13u + 5u * PL : 53u + 5u * (PL / 8u - 1u);
+}
+static_assert(key_used_words(64) == kKeyRecWords, "keying record layout");
 
 // Keying record of the wave-per-record kernel (sg_wpr.hip), u32 words; F26
 // entries are 5 radix-2^26 limbs.  With delta = 0/1 from the geometry

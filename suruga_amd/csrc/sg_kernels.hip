@@ -168,9 +168,10 @@ __device__ __forceinline__ uint32_t mac_lanes(uint32_t n) { return class_mac_lan
 // ---------------------------------------------------------------------------
 // Keying pre-pass: one lane per record.
 // ---------------------------------------------------------------------------
-// The 64 records of a wave are staged in LDS (row stride 97 words: no bank
-// conflicts) and leave as one contiguous 24 KiB run of 16-byte stores; one
-// lane writing its own 384-byte record would touch 64 cache lines per store.
+// The 64 records of a wave are staged in LDS (row stride kKeyRecWords + 1
+// words: no bank conflicts) and leave as one contiguous run of 16-byte stores
+// (skipping the powers a record's class never reads); one lane writing its own
+// record would touch a cache line per store.
 constexpr uint32_t kKeyingThreads = 64;
 
 
@@ -214,17 +215,23 @@ __global__ __launch_bounds__(64) void sg_keying_kernel(const KParams p) {
             R = fmul(R, R);
             if ((g.k >> bit) & 1u) R = fmul(R, r);
         }
+        // only the powers the record's PL MAC lanes read (a prefix of the layout)
+        const uint32_t PL = mac_lanes(n);
+        store_f26(out + key_hi_off(0u), f26_one());
         F26 x = f26_one();
-        for (int j = 0; j < 8; ++j) {  // lo[j] = R^j
-            store_f26(out + kPowLoOff + 5 * j, x);
+        const uint32_t nlo = PL < 8u ? PL : 8u;
+        for (uint32_t j = 0; j < nlo; ++j) {  // lo[j] = R^j
+            store_f26(out + key_lo_off(j), x);
             x = fmul(x, R);
         }
-        const F26 R8 = x;
-        x = f26_one();
-        for (int i = 0; i < 8; ++i) {  // hi[i] = R^(8 i)
-            store_f26(out + kPowHiOff + 5 * i, x);
-            if (i < 7) x = fmul(x, R8);
+        if (PL > 8u) {
+            const F26 R8 = x;
+            for (uint32_t i = 1; i < PL / 8u; ++i) {  // hi[i] = R^(8 i)
+                store_f26(out + key_hi_off(i), x);
+                if (i + 1u < PL / 8u) x = fmul(x, R8);
+            }
         }
+        out[kKeyRecWords] = key_used_words(PL);  // the stage row's pad word
     }
     __syncthreads();
     // coalesced flush: the wave's records are contiguous in the workspace
@@ -235,7 +242,8 @@ __global__ __launch_bounds__(64) void sg_keying_kernel(const KParams p) {
         const uint32_t w = 4u * v;
         const uint32_t rr = w / kKeyRecWords, c = w - rr * kKeyRecWords;
         const uint32_t* src = stage + rr * kKeyLdsStride + c;
-        dst[v] = u32x4{src[0], src[1], src[2], src[3]};
+        if (c < stage[rr * kKeyLdsStride + kKeyRecWords])  // unread powers are not written
+            dst[v] = u32x4{src[0], src[1], src[2], src[3]};
     }
 }
 
@@ -436,8 +444,8 @@ __device__ __forceinline__ void aead_record(const KParams& p, const uint32_t rec
     // combine lanes: total = sum_t h_t R^(PL-1-t), R = r^k; R^e = hi[e >> 3] * lo[e & 7]
     {
         const uint32_t e = PL - 1u - t;
-        const F26 plo = load_f26(kr + kPowLoOff + 5u * (e & 7u));
-        const F26 phi = load_f26(kr + kPowHiOff + 5u * (e >> 3));
+        const F26 plo = load_f26(kr + key_lo_off(e & 7u));
+        const F26 phi = load_f26(kr + key_hi_off(e >> 3));
         const F26 P = mul_add(phi, plo.v0, plo.v1, plo.v2, plo.v3, plo.v4, f26_zero());
         f = mul_add(f, P.v0, P.v1, P.v2, P.v3, P.v4, f26_zero());
     }
@@ -547,7 +555,12 @@ __global__ __launch_bounds__(256) void sg_aead_list_kernel(const KParams p, cons
     const uint32_t g = group_of_thread<L>(), t = threadIdx.x % L;
     const uint32_t cnt = *list_count;
     const uint32_t stride = PERSIST ? gridDim.x * RPW : 0xffffffffu;
-    for (uint32_t base = blockIdx.x * RPW; base < cnt; base += stride) {
+    // XCD-aware order: workgroup b runs on XCD b % 8, and each XCD takes one
+    // contiguous run of the list, so neighbouring records (which share cache
+    // lines: records are packed byte-tight) are fetched by the same L2.
+    const uint32_t nb = gridDim.x, x = blockIdx.x & 7u, q = nb >> 3, r = nb & 7u;
+    const uint32_t wg = x * q + (x < r ? x : r) + (blockIdx.x >> 3);
+    for (uint32_t base = wg * RPW; base < cnt; base += stride) {
         const uint32_t slot = base + g;
         const bool active = slot < cnt;
         uint32_t rec = active ? list[slot] : 0u;
