@@ -68,7 +68,10 @@ def build_library(force: bool = False, out: Path | None = None, defines=()) -> P
         raise ValueError("the product library is built without -D switches; pass out= for a variant")
     if force or defines or _stale(target, HIP_DEPS):
         tmp = target.with_suffix(f".so.tmp{os.getpid()}")  # concurrent builders never share a temp file
+        # no wave-aggregating rewrite of atomics: sg_wpr_kernel's group-counter
+        # fetch must not wait for its return right away (sg_wpr.hip)
         _run([hipcc(), "--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17",
+              "-mllvm", "-amdgpu-atomic-optimizer-strategy=None",
               "-Wall", "-Wno-unused-result", *defines, "-o", str(tmp), *map(str, HIP_SOURCES)])
         os.replace(tmp, target)
     return target

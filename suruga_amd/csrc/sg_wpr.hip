@@ -120,6 +120,7 @@ __global__ __launch_bounds__(64) void sg_wpr_keying_kernel(const KParams p) {
     uint32_t* st = stage + lane * kWprKeyStride;
     const uint32_t adlen = p.tls ? 13u : p.ad_len;
     const WprGeom G = wpr_geom(adlen);
+    if (blockIdx.x == 0u && lane == 0u) p.ws[(uint64_t)p.count * kWprRecWords] = 0u;  // the AEAD kernel's group counter
 
     F26 r = f26_zero();
     uint32_t s[4] = {0u, 0u, 0u, 0u};
@@ -298,7 +299,7 @@ __device__ __forceinline__ F26 reduce_words8(const uint32_t w[8]) {
 #ifndef SG_WPR_PROFILE
 #define SG_WPR_PROFILE 0
 #endif
-constexpr uint32_t kProfPhases = 8, kProfWaves = 4096;
+constexpr uint32_t kProfPhases = 10, kProfWaves = 4096;
 #if SG_WPR_PROFILE
 __device__ unsigned long long g_wpr_prof[kProfWaves][kProfPhases];
 #define SG_TICK(v) const uint64_t v = __builtin_amdgcn_s_memtime()
@@ -388,6 +389,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     auto dma_table_of = [&](uint32_t rec) {  // into the line area
         if (lane < kWprRecWords / 4u) dma_one(lds_lines, p.ws + (uint64_t)rec * kWprRecWords + 4u * lane);
     };
+    // Record groups are handed out dynamically: the first one is the
+    // workgroup's index, every later one comes from a device counter (zeroed by
+    // the keying kernel), fetched by wave 0 at the start of the previous group
+    // and passed to the other waves through LDS.  The two workgroups sharing a
+    // CU do not progress at the same rate (a static g += gridDim.x split left
+    // the fastest waves idle for the last 40 % of the launch).
+    uint32_t* const ctr = p.ws + (uint64_t)p.count * kWprRecWords;
+    uint32_t* const gslot = reinterpret_cast<uint32_t*>(lds + kWprLinesOff + kWprLines * kWprLineBytes + 32u);
     uint32_t g = blockIdx.x;
     if (g < ngroups && g * kWprWaves + wave < p.count) {
         dma_chunk_of(g * kWprWaves + wave, 0u);
@@ -402,9 +411,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
 #if SG_WPR_PROFILE
     uint64_t prof[kProfPhases] = {};
     const uint64_t t_start = __builtin_amdgcn_s_memtime();
+    const uint64_t rt_start = __builtin_amdgcn_s_memrealtime();  // 100 MHz
     uint64_t t_prev = t_start;
 #endif
-    for (; g < ngroups; g += gridDim.x) {
+    while (g < ngroups) {
         SG_TICK(t_rs);
         SG_ACC(7, t_prev, t_rs);  // epilogue + loop overhead of the previous record
 #if SG_WPR_PROFILE
@@ -413,8 +423,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
         const uint32_t rec = g * kWprWaves + wave;
         const bool active = rec < p.count;  // an inactive wave still runs every round and barrier
         const uint32_t recl = rec < p.count ? rec : p.count - 1u;
-        const uint32_t gn = g + gridDim.x, nrec = gn * kWprWaves + wave;
-        const bool next = gn < ngroups && nrec < p.count;
+        uint32_t gn = ngroups, nrec = 0u;  // the next group: known from iteration 3 on
+        bool next = false;
         uint8_t* out = p.out + p.out_stride * recl;
         // key, nonce (chacha20.rs:25-51; TLS: be64(seq), tls.rs:103), received tag
         uint32_t kw[8];
@@ -451,6 +461,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
         else asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
         first = false;
         wave_lds_sync();
+        uint32_t fetched = 0u;
+        if (wave == 0u && lane == 0u)
+            fetched = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         SG_TICK(t_tw);
         SG_ACC(0, t_rs, t_tw);  // wait for the keying table
         const uint32_t* tab = reinterpret_cast<const uint32_t*>(lines);
@@ -577,7 +590,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
             // chunk j has landed in buffer j & 1 (j >= 1: its DMA was the last
             // memory operation of iteration j - 1; j = 0: waited for with the table)
             if (j > 0u) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (j == 1u && wave == 0u && lane == 0u) *gslot = gridDim.x + fetched;  // the atomic has returned
             wave_lds_sync();
+            if (j == 3u) {  // wave 0 published it before the barriers of iterations 1 and 2
+                gn = uniform(*gslot);
+                nrec = gn * kWprWaves + wave;
+                next = gn < ngroups && nrec < p.count;
+            }
             SG_TICK(t_jw);
             SG_ACC(2, t_js, t_jw);  // wait for the chunk
             uint8_t* cb = buf + kWprChunk * (j & 1u);
@@ -758,6 +777,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
                 p.status[rec] = diff != 0u ? 1u : 0u;
             }
         }
+        g = gn;
     }
     if (pend) {  // the last record's last chunk
         wave_lds_sync();
@@ -769,6 +789,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     SG_TICK(t_end);
     SG_ACC(7, t_prev, t_end);
     prof[5] = t_end - t_start;  // the wave's whole life
+    prof[8] = __builtin_amdgcn_s_memrealtime() - rt_start;  // the same in 100 MHz ticks
+    prof[9] = rt_start;
     const uint32_t wid = blockIdx.x * kWprWaves + wave;
     if (lane == 0u && wid < kProfWaves) {
 #pragma unroll

@@ -23,8 +23,9 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT))
 
-PHASES = ["table_wait", "prologue", "chunk_wait", "rounds_mac", "xor_stage_store", "life", "records", "epilogue"]
-NW, NP = 4096, 8
+PHASES = ["table_wait", "prologue", "chunk_wait", "rounds_mac", "xor_stage_store", "life", "records", "epilogue",
+          "realtime", "spare"]
+NW, NP = 4096, 10
 
 
 def main():
@@ -80,12 +81,32 @@ def main():
         res = {"waves": len(rows), "records_per_wave": tot[6] / len(rows),
                "life_cycles_mean": life / len(rows)}
         for k, ph in enumerate(PHASES):
-            if ph in ("life", "records"):
+            if ph in ("life", "records", "realtime", "spare"):
                 continue
             res[ph] = round(tot[k] / life, 4)
+        res["clock_ghz"] = round(tot[5] / tot[8] * 0.1, 3)  # s_memtime ticks per 100 MHz realtime tick
+        t0 = min(r[9] for r in rows)
+        starts = [(r[9] - t0) / 100.0 for r in rows]  # us
+        ends = [(r[9] + r[8] - t0) / 100.0 for r in rows]
+        res["wave_start_us"] = {"max": round(max(starts), 1), "mean": round(sum(starts) / len(starts), 1)}
+        res["wave_end_us"] = {"min": round(min(ends), 1), "mean": round(sum(ends) / len(ends), 1),
+                              "max": round(max(ends), 1)}
+        # by XCD (workgroup b runs on XCD b % 8) and by workgroup-of-the-pair (b // 8 parity)
+        allrows = [buf[w * NP:(w + 1) * NP] for w in range(NW)]
+        by = {}
+        for w, r in enumerate(allrows):
+            if r[5] == 0:
+                continue
+            b = w // 8
+            e = (r[9] + r[8] - t0) / 100.0
+            by.setdefault(("xcd", b % 8), []).append(e)
+            by.setdefault(("half", (b // 256)), []).append(e)
+        res["end_by_group_us"] = {f"{k[0]}{k[1]}": [round(min(v)), round(sum(v) / len(v)), round(max(v))]
+                                  for k, v in sorted(by.items())}
         res["unaccounted"] = round(1 - sum(res[p] for p in PHASES if p in res), 4)
         # per record-group cycles (all waves run the same number of groups)
-        res["cycles_per_group"] = {p: round(tot[k] / tot[6]) for k, p in enumerate(PHASES) if p not in ("life", "records")}
+        res["cycles_per_group"] = {p: round(tot[k] / tot[6]) for k, p in enumerate(PHASES)
+                                   if p not in ("life", "records", "realtime", "spare")}
         out[name] = res
     torch.cuda.synchronize()
     print(json.dumps(out, indent=1))
