@@ -313,7 +313,6 @@ __device__ unsigned long long g_wpr_prof[kProfWaves][kProfPhases];
 // from tools/chacha_grp.inc; every form computes the same rounds)
 #ifndef SG_WPR_DR_ASM
 #define SG_WPR_DR_ASM SG_CHACHA_DR_NB1_BAR1
-#define SG_WPR_DR1_ASM SG_CHACHA_DR1_NB1_BAR1
 #endif
 
 // A zero vector materialised where it is used (a hoisted constant would hold
@@ -449,6 +448,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
         uint32_t u[16] = {kSigma0, kSigma1, kSigma2, kSigma3, kw[0], kw[1], kw[2], kw[3],
                           kw[4],   kw[5],   kw[6],   kw[7],   0u,    0u,    n14,   n15};
         SG_QR(u[1], u[5], u[9], u[13]) SG_QR(u[2], u[6], u[10], u[14]) SG_QR(u[3], u[7], u[11], u[15])
+        // and the steps of the double round whose operands are all uniform
+        // (tools/gen_chacha_grp.py, SG_CHACHA_DR1S_*; tests/test_chacha_asm_model.py)
+        const uint32_t S0 = u[0] + u[4], T1 = u[1] + u[6], T2 = u[2] + u[7];
+        const uint32_t T13 = rotl32(u[13] ^ T2, 16);
         uint32_t rx[4] = {0u, 0u, 0u, 0u};
         if constexpr (OPEN) {  // the received tag (chacha20_poly1305.rs:72-73)
             const uint8_t* tg = p.in + p.in_stride * recl + kWprN;
@@ -577,11 +580,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
                  : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]), "+v"(x[7]), \
                    "+v"(x[8]), "+v"(x[9]), "+v"(x[10]), "+v"(x[11]), "+v"(x[12]), "+v"(x[13]), "+v"(x[14]),         \
                    "+v"(x[15]))
-#define SG_DR1()                                                                                                  \
-    asm volatile(SG_WPR_DR1_ASM                                                                                   \
-                 : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]), "+v"(x[7]), \
-                   "+v"(x[8]), "+v"(x[9]), "+v"(x[10]), "+v"(x[11]), "+v"(x[12]), "+v"(x[13]), "+v"(x[14]),         \
-                   "+v"(x[15]))
 #define SG_PIN() __builtin_amdgcn_sched_barrier(0)
 
 #pragma unroll
@@ -604,11 +602,19 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
 
             // keystream block 64 j + lane + 1 (chacha20_poly1305.rs:52), lock-step rounds
             const uint32_t ctr = 64u * j + lane + 1u;
-            uint32_t x[16] = {kSigma0, u[1], u[2], u[3], kw[0], u[5], u[6],  u[7],
-                              kw[4],   u[9], u[10], u[11], ctr,  u[13], u[14], u[15]};
+            uint32_t x[16];
+            x[12] = ctr;
             u32x4 D[4];
             SG_PIN();
-            SG_DR1();
+            // first double round: every word but the counter enters from SGPRs
+            asm volatile(SG_CHACHA_DR1S_COL : "=v"(x[0]), "=v"(x[4]), "=v"(x[8]), "+v"(x[12])
+                         : "s"(S0), "s"(kw[0]), "s"(kw[4]));
+            asm volatile(SG_CHACHA_DR1S_DIAG
+                         : "+v"(x[0]), "+v"(x[4]), "+v"(x[8]), "+v"(x[12]), "=v"(x[1]), "=v"(x[2]), "=v"(x[3]),
+                           "=v"(x[5]), "=v"(x[6]), "=v"(x[7]), "=v"(x[9]), "=v"(x[10]), "=v"(x[11]), "=v"(x[13]),
+                           "=v"(x[14]), "=v"(x[15])
+                         : "s"(u[5]), "s"(u[15]), "s"(T1), "s"(u[3]), "s"(u[14]), "s"(u[10]), "s"(u[11]), "s"(T13),
+                           "s"(u[9]), "s"(u[6]), "s"(u[7]), "s"(T2));
             SG_PIN();
             // The previous chunk's output leaves lane-contiguously one 1 KiB piece
             // per double round (read from LDS one gap ahead of its store), and
@@ -737,7 +743,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
 #endif
         }
 #undef SG_DR
-#undef SG_DR1
 #undef SG_PIN
 
         // ---- assemble X = sum_r D[c_r][q] 2^(8 c_r - 32 hh), c_r = (r & 3) + 8 (r >> 2) + 4 hh
