@@ -2,23 +2,26 @@
 // records (klutzy/suruga src/cipher/chacha20_poly1305.rs:48-94 on records of
 // RECORD_MAX_LEN = 2^14 bytes, tls.rs:32,137-147).
 //
-// One wave owns one record; a 512-thread workgroup holds eight records (two
-// waves per SIMD) and walks record groups persistently.  Per record the wave
-// runs four iterations over 4 KiB chunks:
+// One wave owns one record; a 512-thread workgroup holds eight records, two
+// workgroups share a CU (four waves per SIMD), and the persistent grid takes
+// record groups from a device counter.  Per record the wave runs four
+// iterations over 4 KiB chunks:
 //
-//   * the chunk arrives lane-contiguously (16 B per lane, 1 KiB per load
-//     instruction, prefetched one chunk ahead into registers) and is staged in
-//     the wave's LDS slice through an XOR swizzle, so that lane t then reads
-//     its own 64-byte block 64 j + t conflict-free;
+//   * the chunk arrives by LDS-DMA, lane-contiguously (16 B per lane, 1 KiB
+//     per instruction, prefetched one chunk ahead, one piece per double round)
+//     into the wave's LDS slice through an XOR swizzle, so that lane t then
+//     reads its own 64-byte block 64 j + t conflict-free;
 //   * lane t computes keystream block 64 j + t + 1 (chacha20.rs:111-135, block
 //     0 being the Poly1305 key, chacha20_poly1305.rs:50-52) with grouped ARX
 //     rounds and an s_barrier after every rotate group (sg_chacha_grp.inc),
-//     which keeps the two waves of each SIMD in lock-step so that their
-//     full-rate add/xor instructions pair up;
-//   * the XOR result leaves through the same swizzled slice, lane-contiguously;
+//     which keeps the waves of each SIMD in lock-step so that their full-rate
+//     add/xor instructions pair up;
+//   * the XOR result is staged in the same swizzled slice and leaves
+//     lane-contiguously during the next chunk's first double rounds;
 //   * Poly1305 is fed from the ciphertext registers themselves: the wave's 64
 //     lanes hold 256 consecutive 16-byte ciphertext chunks, which are the B
-//     operands of four v_mfma_i32_32x32x32_i8 per iteration (see "MAC" below).
+//     operands of four v_mfma_i32_32x32x32_i8 per iteration, issued during the
+//     next iteration's rounds (see "MAC" below).
 //
 // MAC.  The reference evaluates h = sum_b v_b r^(B - b) over the 16-byte
 // blocks of ad || le64(|ad|) || ct || le64(|ct|) (chacha20_poly1305.rs:19-42,
@@ -34,7 +37,8 @@
 // digits of r^(e + 1) and r^e, shifted by sigma + a' (a Toeplitz band).  The
 // eight powers per step, r^(128 k + 1 + delta + u) (k = 0..7, u = 0..4), are
 // built once per record as 48-byte digit lines in LDS; a lane reads its
-// 16-byte T fragment as two unaligned windows of two adjacent lines.  |D| <
+// 16-byte T fragment as two windows of two adjacent lines (aligned dwords
+// shifted with v_alignbyte).  |D| <
 // 2^23, so with the accumulator seeded at 2^24 every entry is a positive
 // 25-bit integer.  At the end each lane assembles its 16 entries exactly,
 // X = sum_r D[c_r][q] 2^(8 c_r), reduces it mod 2^130 - 5, multiplies by
@@ -872,10 +876,11 @@ int set_wpr(int enable) {
 }
 
 const char* wpr_kernel_config() {
-    return "sg_wpr_kernel v13: full 16 KiB records, one wave per record (8 per 512-thread workgroup, persistent "
-           "2 per CU), 4 KiB chunks LDS-DMA prefetched lane-contiguously into an XOR-swizzled LDS slice, output "
+    return "sg_wpr_kernel v14: full 16 KiB records, one wave per record (8 per 512-thread workgroup, persistent "
+           "2 per CU, record groups handed out by a device counter), 4 KiB chunks LDS-DMA prefetched lane-contiguously into an XOR-swizzled LDS slice, output "
            "read out during the next chunk's first double rounds, lock-step grouped ChaCha20 rounds (s_barrier per "
-           "rotate group; counter-free first column quarter rounds once per record on the SALU), Poly1305 as 16 "
+           "rotate group; the first double round takes its uniform words from SGPRs, the counter-free steps once "
+           "per record on the SALU), Poly1305 as 16 "
            "v_mfma_i32_32x32x32_i8 per record fed from the ciphertext registers one chunk behind (Toeplitz digit "
            "lines of r^(128k+d) in LDS, read as aligned dwords + v_alignbyte), exact per-lane assembly, "
            "W = r^(4(31-q)) scaling, DPP sum; keying pre-pass with the constant term";
