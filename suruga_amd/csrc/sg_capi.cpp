@@ -221,8 +221,17 @@ int launch_batch(const sg_batch* b, bool open, hipStream_t s, void* ws) {
     const uint32_t max_n = open ? (maxl >= 16u ? maxl - 16u : 0u) : maxl;
     const bool uniform = !b->len || sg::size_class(max_n) == 0u;
     const bool wpr = wpr_eligible(b, open);
-    uint32_t* lists = p.ws + (size_t)b->count * sg::kKeyRecWordsMax;
-    uint32_t* counts = lists + (uint64_t)sg::kNumClasses * b->count;
+    // mixed TLS batches: full-chunk records (4-16 KiB, multiples of 64 bytes)
+    // go to the wave-per-record buckets; not under capture (they are launched
+    // on the populations read back), and the per-record arrays are read as
+    // dwords by the bucket kernels
+    if (!wpr && !uniform && p.tls && sg::wpr_enabled() && max_n > 4096u) {
+        hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+        SG_HIP(hipStreamIsCapturing(s, &cap));
+        p.wpr_mix = cap == hipStreamCaptureStatusNone &&
+                    ((uintptr_t)b->key_index | (uintptr_t)b->seq | (uintptr_t)b->len | (uintptr_t)b->in_off |
+                     (uintptr_t)b->out_off) % 4u == 0u;
+    }
 
     hipEvent_t e[4] = {nullptr, nullptr, nullptr, nullptr};
     bool timing = false;
@@ -236,13 +245,8 @@ int launch_batch(const sg_batch* b, bool open, hipStream_t s, void* ws) {
     if (wpr) {
         SG_HIP(sg::launch_wpr(p, open, s, timing ? e[1] : nullptr, timing ? e[2] : nullptr));
     } else {
-        SG_HIP(sg::launch_keying(p, open, s));
-        if (timing) {
-            SG_HIP(hipEventRecord(e[1], s));
-            SG_HIP(hipEventRecord(e[2], s));
-        }
         uint32_t over = 0;
-        SG_HIP(sg::launch_aead(p, open, max_n, uniform, lists, counts, s, &over));
+        SG_HIP(sg::launch_aead(p, open, max_n, uniform, s, &over, timing ? e[1] : nullptr, timing ? e[2] : nullptr));
         if (over) return fail(SG_E_ARG, "records longer than max_len were not processed%s");
     }
     if (timing) {
@@ -315,7 +319,7 @@ const char* sg_build_info(void) {
 size_t sg_workspace_size(uint32_t count) {
     // keying records, one list per size class, the class populations and the
     // count of records longer than max_len
-    return (size_t)count * (sg::kKeyRecWordsMax + sg::kNumClasses) * 4u + (sg::kNumClasses + 1u) * 4u;
+    return (size_t)sg::ws_words(count) * 4u;
 }
 
 sg_ctx* sg_ctx_new(const uint8_t key[32], int device) {

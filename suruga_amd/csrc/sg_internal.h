@@ -40,7 +40,10 @@ constexpr uint32_t kWTk = 40;
 constexpr uint32_t kWLo = 80;
 constexpr uint32_t kWHi = 120;
 constexpr uint32_t kWprRecWords = 160;
-constexpr uint32_t kKeyRecWordsMax = kWprRecWords;
+// Record descriptor of a listed wave-per-record record (mixed batches), u32
+// words, indexed like the keying records by the record's slot in its bucket:
+//   in_off[2] out_off[2] n rec key_index n14 n15 0 0 0
+constexpr uint32_t kWprDescWords = 12;
 
 // Kernel parameters (passed by value as kernarg).
 struct KParams {
@@ -66,6 +69,7 @@ struct KParams {
     uint32_t tls;            // 1 = SG_BATCH_TLS
     uint32_t tls_hdr;        // content_type | major << 8 | minor << 16
     uint32_t lds_rec_bytes;  // LDS bytes per record slot of the launched size class
+    uint32_t wpr_mix;        // mixed batch: route eligible records to the wave-per-record buckets
 };
 
 // Size classes of the AEAD kernel: class c (0..7) holds records of
@@ -74,6 +78,12 @@ struct KParams {
 // c < 7; the MAC runs on PL = min(L, 64) lanes.  A 256-thread workgroup serves
 // 256 / L records.  Mixed sizes are bucketed on the device (sg_classify_kernel).
 constexpr uint32_t kNumClasses = 8;
+// Mixed batches also route TLS records of 4 KiB < n <= 16 KiB, n a multiple of
+// 64, 16-byte aligned, to the wave-per-record kernel (sg_wpr.hip): bucket
+// J = ceil(n / 4096) = 2..4 (the record's chunk count), lists kNumClasses + J - 2.
+constexpr uint32_t kWprBuckets = 3;
+constexpr uint32_t kWprMinJ = 2;
+constexpr uint32_t kNumLists = kNumClasses + kWprBuckets;
 constexpr uint32_t kListGridPerCU = 8;   // workgroups per CU for list-driven launches
 
 __host__ __device__ inline uint32_t size_class(uint32_t n) {
@@ -96,21 +106,68 @@ __host__ __device__ inline uint32_t lds_rec_bytes(uint32_t cls, uint32_t adlen, 
 // gives every record but a stream's tail), 16-byte aligned strided layout, any
 // AD length.  One wave per record, eight records per 512-thread workgroup.
 constexpr uint32_t kWprN = 16384;
+// Workspace (u32 words) for a batch of `count` records:
+//   [0, 88 count)                   size-class keying records (by record index)
+//   [88 count, 248 count)           wave-per-record keying records (by slot)
+//   [248 count, 260 count)          wave-per-record descriptors (by slot)
+//   [260 count, 271 count)          kNumLists record lists
+//   then kNumLists populations, the over-long count, kWprBuckets + 1 group counters
+constexpr uint32_t kWsWprTab = kKeyRecWords;
+constexpr uint32_t kWsWprDesc = kWsWprTab + kWprRecWords;
+constexpr uint32_t kWsLists = kWsWprDesc + kWprDescWords;
+constexpr uint32_t kWsRecWords = kWsLists + kNumLists;
+constexpr uint32_t kWsTailWords = kNumLists + 1u + kWprBuckets + 1u;
+__host__ __device__ inline uint64_t ws_words(uint32_t count) { return (uint64_t)count * kWsRecWords + kWsTailWords; }
+// the counts / counters tail
+__host__ __device__ inline uint32_t* ws_tail(uint32_t* ws, uint32_t count) { return ws + (uint64_t)count * kWsRecWords; }
+constexpr uint32_t kTailOver = kNumLists;           // records longer than max_n
+constexpr uint32_t kTailCtr = kNumLists + 1u;       // + b: group counter of wpr bucket b, + kWprBuckets: uniform C1 launch
+
+// A wave-per-record bucket launch (mixed batch) or the uniform launch (list NULL).
+struct WprList {
+    const uint32_t* list;    // record indices (bucket list) or NULL: slot = record
+    uint32_t count;          // records in the launch
+    uint32_t* tab;           // keying records, kWprRecWords per slot
+    uint32_t* desc;          // descriptors, kWprDescWords per slot (list launches)
+    uint32_t* ctr;           // the launch's group counter (zeroed by its keying kernel)
+};
+
+// Keying jobs of the size-class keying kernel: njobs == 0 keys every record
+// of the batch by index, otherwise the records of the listed size classes.
+struct KeyJobs {
+    const uint32_t* list[kNumClasses];
+    uint32_t count[kNumClasses];
+    uint32_t blk0[kNumClasses];  // first 64-record block of each job
+    uint32_t njobs;
+};
+
 bool wpr_enabled();  // sg_set_lockstep / SG_LOCKSTEP environment switch
 int set_wpr(int enable);
 // keying pre-pass + record kernel; ev_mid (may be NULL) is recorded between them
 hipError_t launch_wpr(const KParams& p, bool open, hipStream_t s, hipEvent_t ev_keyed, hipEvent_t ev_start);
+// wave-per-record buckets of a mixed batch (wl[b]: J = kWprMinJ + b chunks):
+// one keying launch for every bucket, then the record kernel of one bucket
+hipError_t launch_wpr_keying_lists(const KParams& p, bool open, const WprList* wl, hipStream_t s);
+hipError_t launch_wpr_list(const KParams& p, bool open, uint32_t J, const WprList& wl, hipStream_t s);
 const char* wpr_kernel_config();
 const char* class_kernel_config();
 
-hipError_t launch_keying(const KParams& p, bool open, hipStream_t s);
-// Seal/open launch.  uniform: every record is in size_class(max_n) (direct
-// launch); otherwise classify into lists[kNumClasses][count] / counts[kNumClasses] and
-// launch per class.  counts has kNumClasses + 1 words: the last counts the
-// records longer than max_n, which are skipped (open: status 3); *over
-// receives that count when the populations are read back (not under capture).
-hipError_t launch_aead(const KParams& p, bool open, uint32_t max_n, bool uniform, uint32_t* lists,
-                       uint32_t* counts, hipStream_t s, uint32_t* over);
+// Seal/open launch of a batch that is not a uniform 16 KiB one.  uniform:
+// every record is in size_class(max_n) (keying, direct launch); otherwise
+// classify into the workspace lists (kNumLists x count, populations in the
+// tail), key the listed records and launch per list: the wave-per-record
+// buckets (p.wpr_mix) first, then the size classes.  The tail's over-long count receives the records
+// longer than max_n, which are skipped (open: status 3); *over receives that
+// count when the populations are read back (not under capture).
+// ev_keyed / ev_start (may be NULL) are recorded after the keying pre-passes
+hipError_t launch_aead(const KParams& p, bool open, uint32_t max_n, bool uniform, hipStream_t s, uint32_t* over,
+                       hipEvent_t ev_keyed, hipEvent_t ev_start);
+// Eligibility of one record of a mixed batch for the wave-per-record buckets:
+// the bucket J (kWprMinJ..4) or 0.  Shared by the classify and keying kernels.
+__host__ __device__ inline uint32_t wpr_bucket_of(uint32_t n, uint64_t in_addr, uint64_t out_addr) {
+    if (n <= 4096u || n > kWprN || (n & 63u) || ((in_addr | out_addr) & 15u)) return 0u;
+    return (n + 4095u) >> 12;
+}
 hipError_t launch_fill(uint8_t* buf, uint64_t stride, uint32_t len, uint32_t count, uint64_t seed,
                        uint64_t j0, hipStream_t s);
 hipError_t launch_compare(const uint8_t* a, uint64_t sa, const uint8_t* b, uint64_t sb, uint32_t len,

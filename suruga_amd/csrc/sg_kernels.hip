@@ -174,22 +174,48 @@ __device__ __forceinline__ uint32_t mac_lanes(uint32_t n) { return class_mac_lan
 // record would touch a cache line per store.
 constexpr uint32_t kKeyingThreads = 64;
 
+// The wave-per-record bucket of record rec of a mixed batch (0: a size class);
+// n is the plaintext length.  The classify and keying kernels agree on it.
+__device__ __forceinline__ uint32_t rec_wpr_bucket(const KParams& p, uint32_t rec, uint32_t n) {
+    if (!p.wpr_mix) return 0u;
+    const uint64_t ia = (uint64_t)(uintptr_t)p.in + (p.in_off ? p.in_off[rec] : p.in_stride * rec);
+    const uint64_t oa = (uint64_t)(uintptr_t)p.out + (p.out_off ? p.out_off[rec] : p.out_stride * rec);
+    return wpr_bucket_of(n, ia, oa);
+}
+
 
 // Keying pre-pass of the size-class kernels: ChaCha20 block 0 -> Poly1305 key
 // (chacha20_poly1305.rs:50,75,32-39; r clamped as poly1305.rs:197-203), and
 // with R = r^k (k = MAC blocks per lane, mac_geom) the tables R^0..R^7 and
 // R^0, R^8, .., R^56 that scale the MAC lanes' partial sums.
+// KeyJobs (sg_internal.h): njobs == 0 keys every record of the batch by
+// index; otherwise the records of up to kNumClasses lists (mixed batches key
+// only their size-class records here), job i on blocks [blk0[i], blk0[i+1]).
 template <bool OPEN>
-__global__ __launch_bounds__(64) void sg_keying_kernel(const KParams p) {
+__global__ __launch_bounds__(64) void sg_keying_kernel(const KParams p, const KeyJobs jobs) {
     constexpr uint32_t kKeyLdsStride = kKeyRecWords + 1;
     __shared__ uint32_t stage[kKeyingThreads * kKeyLdsStride];
+    __shared__ uint32_t recs[kKeyingThreads];
     const uint32_t lane = threadIdx.x;
-    const uint32_t rec0 = blockIdx.x * kKeyingThreads;
-    const uint32_t rec = rec0 + lane;
+    const uint32_t* list = nullptr;
+    uint32_t cnt = p.count, b0 = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < kNumClasses; ++i)  // (constant indices: the kernarg table stays in SGPRs)
+        if (i < jobs.njobs && blockIdx.x >= jobs.blk0[i]) {
+            list = jobs.list[i];
+            cnt = jobs.count[i];
+            b0 = jobs.blk0[i];
+        }
+    const uint32_t slot0 = (blockIdx.x - b0) * kKeyingThreads;
+    const uint32_t slot = slot0 + lane;
+    const bool act = slot < cnt;
+    const uint32_t rec = act ? (list ? list[slot] : slot) : 0u;
+    recs[lane] = rec;
     uint32_t* out = stage + lane * kKeyLdsStride;
-    if (rec < p.count) {
-        const uint32_t len = record_len(p, rec);
-        const uint32_t n = OPEN ? (len >= 16u ? len - 16u : 0u) : len;
+    const uint32_t len = act ? record_len(p, rec) : 0u;
+    const uint32_t n = OPEN ? (len >= 16u ? len - 16u : 0u) : len;
+    out[kKeyRecWords] = 0u;  // nothing to write unless keyed below
+    if (act) {
         const RecKey rk = record_key(p, rec);
         uint32_t ks[16];
         chacha_block(ks, rk.k, 0u, rk.n14, rk.n15);  // block 0 -> poly key (chacha20_poly1305.rs:50)
@@ -234,16 +260,16 @@ __global__ __launch_bounds__(64) void sg_keying_kernel(const KParams p) {
         out[kKeyRecWords] = key_used_words(PL);  // the stage row's pad word
     }
     __syncthreads();
-    // coalesced flush: the wave's records are contiguous in the workspace
-    const uint32_t nrec = p.count - rec0 < kKeyingThreads ? p.count - rec0 : kKeyingThreads;
-    u32x4* dst = reinterpret_cast<u32x4*>(p.ws + (uint64_t)rec0 * kKeyRecWords);
+    // coalesced flush: 16-byte stores of consecutive words of a record
+    // (records by index are contiguous in the workspace; listed ones are not)
+    const uint32_t nrec = cnt - slot0 < kKeyingThreads ? cnt - slot0 : kKeyingThreads;
     const uint32_t nvec = nrec * (kKeyRecWords / 4u);
     for (uint32_t v = lane; v < nvec; v += kKeyingThreads) {
         const uint32_t w = 4u * v;
         const uint32_t rr = w / kKeyRecWords, c = w - rr * kKeyRecWords;
         const uint32_t* src = stage + rr * kKeyLdsStride + c;
         if (c < stage[rr * kKeyLdsStride + kKeyRecWords])  // unread powers are not written
-            dst[v] = u32x4{src[0], src[1], src[2], src[3]};
+            *reinterpret_cast<u32x4*>(p.ws + (uint64_t)recs[rr] * kKeyRecWords + c) = u32x4{src[0], src[1], src[2], src[3]};
     }
 }
 
@@ -355,8 +381,16 @@ __device__ __forceinline__ void aead_record(const KParams& p, const uint32_t rec
     if (!work || t >= PL) return;
 
     // ---- phase 2: Poly1305 on PL lanes -----------------------------------------
-    // open: the finishing lane fetches the received tag now so that its memory latency
-    // hides behind the Horner loop instead of stalling the final compare
+    const MacGeom g = mac_geom(adlen, n, PL);
+    const uint32_t* kr = p.ws + (uint64_t)rec * kKeyRecWords;
+    uint32_t r0 = kr[kR32Off + 0], r1 = kr[kR32Off + 1], r2 = kr[kR32Off + 2], r3 = kr[kR32Off + 3];
+    if constexpr (PL == 64u) {  // one record per wave: keep the key in SGPRs
+        r0 = uniform(r0); r1 = uniform(r1); r2 = uniform(r2); r3 = uniform(r3);
+    }
+    const uint32_t s1 = r1 + (r1 >> 2), s2 = r2 + (r2 >> 2), s3 = r3 + (r3 >> 2);
+    // open: the finishing lane fetches the received tag after the keying record's r
+    // words (loads retire in order: waiting for r must not wait for the tag), so
+    // that its latency hides behind the Horner loop
     uint32_t rx[4] = {0u, 0u, 0u, 0u};
     if constexpr (OPEN) {
         if (t == PL - 1u) {  // the lane that finishes the tag
@@ -370,13 +404,6 @@ __device__ __forceinline__ void aead_record(const KParams& p, const uint32_t rec
             }
         }
     }
-    const MacGeom g = mac_geom(adlen, n, PL);
-    const uint32_t* kr = p.ws + (uint64_t)rec * kKeyRecWords;
-    uint32_t r0 = kr[kR32Off + 0], r1 = kr[kR32Off + 1], r2 = kr[kR32Off + 2], r3 = kr[kR32Off + 3];
-    if constexpr (PL == 64u) {  // one record per wave: keep the key in SGPRs
-        r0 = uniform(r0); r1 = uniform(r1); r2 = uniform(r2); r3 = uniform(r3);
-    }
-    const uint32_t s1 = r1 + (r1 >> 2), s2 = r2 + (r2 >> 2), s3 = r3 + (r3 >> 2);
 
     // lane t: virtual blocks [t*k, t*k + k); virtual block v is real iff v >= z
     const uint32_t v0 = t * g.k;
@@ -581,33 +608,35 @@ constexpr uint32_t kClassifyPerThread = 4;
 template <bool OPEN>
 __global__ __launch_bounds__(1024) void sg_classify_kernel(const KParams p, uint32_t* __restrict__ lists,
                                                            uint32_t* __restrict__ counts, const uint32_t max_n) {
-    __shared__ uint32_t wave_cnt[kNumClasses][kClassifyThreads / 64];
-    __shared__ uint32_t wg_base[kNumClasses];
+    // counts: the kNumLists populations, then the over-long count
+    __shared__ uint32_t wave_cnt[kNumLists][kClassifyThreads / 64];
+    __shared__ uint32_t wg_base[kNumLists];
     const uint32_t lane = __lane_id(), wave = threadIdx.x >> 6;
     const uint32_t rec0 = blockIdx.x * (kClassifyThreads * kClassifyPerThread);
     uint32_t cls[kClassifyPerThread];
-    uint32_t mine[kNumClasses] = {};  // this wave's records per class
+    uint32_t mine[kNumLists] = {};  // this wave's records per list
 #pragma unroll
     for (uint32_t i = 0; i < kClassifyPerThread; ++i) {
         const uint32_t rec = rec0 + i * kClassifyThreads + threadIdx.x;
-        cls[i] = kNumClasses;
+        cls[i] = kNumLists;
         if (rec < p.count) {
             const uint32_t len = record_len(p, rec);
             const uint32_t n = OPEN ? (len >= 16u ? len - 16u : 0u) : len;
             if (n <= max_n) {
-                cls[i] = size_class(n);
+                const uint32_t J = rec_wpr_bucket(p, rec, n);
+                cls[i] = J ? kNumClasses + J - kWprMinJ : size_class(n);
             } else {  // longer than the batch's max_len: no class (its LDS slot would overflow), flagged
-                atomicAdd(&counts[kNumClasses], 1u);
+                atomicAdd(&counts[kNumLists], 1u);
                 if constexpr (OPEN) p.status[rec] = 3u;
             }
         }
 #pragma unroll
-        for (uint32_t c = 0; c < kNumClasses; ++c) mine[c] += (uint32_t)__popcll(__ballot(cls[i] == c));
+        for (uint32_t c = 0; c < kNumLists; ++c) mine[c] += (uint32_t)__popcll(__ballot(cls[i] == c));
     }
     if (lane == 0)
-        for (uint32_t c = 0; c < kNumClasses; ++c) wave_cnt[c][wave] = mine[c];
+        for (uint32_t c = 0; c < kNumLists; ++c) wave_cnt[c][wave] = mine[c];
     __syncthreads();
-    if (threadIdx.x < kNumClasses) {
+    if (threadIdx.x < kNumLists) {
         uint32_t tot = 0;
         for (uint32_t w = 0; w < kClassifyThreads / 64; ++w) {
             const uint32_t x = wave_cnt[threadIdx.x][w];
@@ -617,14 +646,14 @@ __global__ __launch_bounds__(1024) void sg_classify_kernel(const KParams p, uint
         wg_base[threadIdx.x] = tot ? atomicAdd(&counts[threadIdx.x], tot) : 0u;
     }
     __syncthreads();
-    uint32_t off[kNumClasses];
+    uint32_t off[kNumLists];
 #pragma unroll
-    for (uint32_t c = 0; c < kNumClasses; ++c) off[c] = wg_base[c] + wave_cnt[c][wave];
+    for (uint32_t c = 0; c < kNumLists; ++c) off[c] = wg_base[c] + wave_cnt[c][wave];
 #pragma unroll
     for (uint32_t i = 0; i < kClassifyPerThread; ++i) {
         const uint32_t rec = rec0 + i * kClassifyThreads + threadIdx.x;
 #pragma unroll
-        for (uint32_t c = 0; c < kNumClasses; ++c) {
+        for (uint32_t c = 0; c < kNumLists; ++c) {
             const uint64_t mask = __ballot(cls[i] == c);
             if (cls[i] == c) lists[(uint64_t)c * p.count + off[c] + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull))] = rec;
             off[c] += (uint32_t)__popcll(mask);
@@ -688,14 +717,22 @@ __global__ __launch_bounds__(256) void sg_compare_kernel(const uint8_t* a, uint6
 
 }  // namespace
 
-hipError_t launch_keying(const KParams& p, bool open, hipStream_t s) {
-    const uint32_t grid = (p.count + kKeyingThreads - 1u) / kKeyingThreads;
+static hipError_t launch_keying(const KParams& p, bool open, const KeyJobs& jobs, uint32_t grid, hipStream_t s) {
+    if (grid == 0) return hipSuccess;
     if (open)
-        hipLaunchKernelGGL((sg_keying_kernel<true>), dim3(grid), dim3(kKeyingThreads), 0, s, p);
+        hipLaunchKernelGGL((sg_keying_kernel<true>), dim3(grid), dim3(kKeyingThreads), 0, s, p, jobs);
     else
-        hipLaunchKernelGGL((sg_keying_kernel<false>), dim3(grid), dim3(kKeyingThreads), 0, s, p);
+        hipLaunchKernelGGL((sg_keying_kernel<false>), dim3(grid), dim3(kKeyingThreads), 0, s, p, jobs);
     return hipGetLastError();
 }
+
+// every record of the batch, by index
+static hipError_t launch_keying_all(const KParams& p, bool open, hipStream_t s) {
+    KeyJobs jobs = {};
+    return launch_keying(p, open, jobs, (p.count + kKeyingThreads - 1u) / kKeyingThreads, s);
+}
+
+static hipError_t mark(hipEvent_t ev, hipStream_t s) { return ev ? hipEventRecord(ev, s) : hipSuccess; }
 
 template <bool OPEN, uint32_t L>
 hipError_t launch_direct(const KParams& p, hipStream_t s) {
@@ -742,49 +779,92 @@ hipError_t launch_class(uint32_t c, const KParams& q, const uint32_t* list, cons
 }
 
 template <bool OPEN>
-hipError_t launch_aead_t(const KParams& p, uint32_t max_n, bool uniform, uint32_t* lists, uint32_t* counts,
-                         hipStream_t s, uint32_t* over) {
+hipError_t launch_aead_t(const KParams& p, uint32_t max_n, bool uniform, hipStream_t s, uint32_t* over,
+                         hipEvent_t ev_keyed, hipEvent_t ev_start) {
     *over = 0;
-    if (uniform) {  // every record in one class: direct launch
+    hipError_t e;
+    if (uniform) {  // every record in one class: keying, then a direct launch
+        if ((e = launch_keying_all(p, OPEN, s)) != hipSuccess || (e = mark(ev_keyed, s)) != hipSuccess ||
+            (e = mark(ev_start, s)) != hipSuccess)
+            return e;
         KParams q = p;
         const uint32_t c = size_class(max_n);
         q.lds_rec_bytes = lds_rec_bytes(c, q.ad_len, max_n);
         return launch_class<OPEN>(c, q, nullptr, nullptr, 0, s);
     }
-    hipError_t e = hipMemsetAsync(counts, 0, (kNumClasses + 1u) * sizeof(uint32_t), s);
-    if (e != hipSuccess) return e;
+    uint32_t* const tail = ws_tail(p.ws, p.count);
+    uint32_t* const lists = p.ws + (uint64_t)p.count * kWsLists;
+    if ((e = hipMemsetAsync(tail, 0, (kNumLists + 1u) * sizeof(uint32_t), s)) != hipSuccess) return e;
     const uint32_t per_wg = kClassifyThreads * kClassifyPerThread;
     hipLaunchKernelGGL(sg_classify_kernel<OPEN>, dim3((p.count + per_wg - 1u) / per_wg), dim3(kClassifyThreads), 0, s,
-                       p, lists, counts, max_n);
+                       p, lists, tail, max_n);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    // Read the class populations back (one stream sync per mixed batch) so every
-    // class runs on an exact grid; under stream capture the host cannot wait,
-    // so the classes run on persistent grids instead.
-    uint32_t pop[kNumClasses + 1];
+    // Read the list populations back (one stream sync per mixed batch) so that
+    // the keying kernels run over exactly the listed records and every list
+    // on an exact grid; under stream capture the host cannot wait, so every
+    // record is keyed and the classes run on persistent grids instead (and the
+    // caller leaves p.wpr_mix off: the wave-per-record buckets need their
+    // populations).
+    uint32_t pop[kNumLists + 1];
     hipStreamCaptureStatus cap_status = hipStreamCaptureStatusNone;
     if ((e = hipStreamIsCapturing(s, &cap_status)) != hipSuccess) return e;
     const bool exact = cap_status == hipStreamCaptureStatusNone;
     if (exact) {
-        if ((e = hipMemcpyAsync(pop, counts, sizeof pop, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+        if ((e = hipMemcpyAsync(pop, tail, sizeof pop, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
         if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+        *over = pop[kTailOver];
+        // size-class keying over the class lists only
+        KeyJobs jobs = {};
+        uint32_t grid = 0;
+        for (uint32_t c = 0; c < kNumClasses; ++c) {
+            if (pop[c] == 0) continue;
+            jobs.list[jobs.njobs] = lists + (uint64_t)c * p.count;
+            jobs.count[jobs.njobs] = pop[c];
+            jobs.blk0[jobs.njobs] = grid;
+            grid += (pop[c] + kKeyingThreads - 1u) / kKeyingThreads;
+            ++jobs.njobs;
+        }
+        if ((e = launch_keying(p, OPEN, jobs, grid, s)) != hipSuccess) return e;
+    } else if ((e = launch_keying_all(p, OPEN, s)) != hipSuccess) {
+        return e;
     }
-    if (exact) *over = pop[kNumClasses];
+    // wave-per-record buckets (J = 2..4 chunks): their keying records and
+    // descriptors are packed by slot in bucket order
+    WprList wl[kWprBuckets] = {};
+    if (p.wpr_mix && exact) {
+        uint64_t base = 0;
+        for (uint32_t b = 0; b < kWprBuckets; ++b) {
+            const uint32_t nb = pop[kNumClasses + b];
+            wl[b].list = lists + (uint64_t)(kNumClasses + b) * p.count;
+            wl[b].count = nb;
+            wl[b].tab = p.ws + (uint64_t)p.count * kWsWprTab + base * kWprRecWords;
+            wl[b].desc = p.ws + (uint64_t)p.count * kWsWprDesc + base * kWprDescWords;
+            wl[b].ctr = tail + kTailCtr + b;
+            base += nb;
+        }
+        if ((e = launch_wpr_keying_lists(p, OPEN, wl, s)) != hipSuccess) return e;
+    }
+    if ((e = mark(ev_keyed, s)) != hipSuccess || (e = mark(ev_start, s)) != hipSuccess) return e;
+    if (p.wpr_mix && exact) {  // most chunks first
+        for (int b = (int)kWprBuckets - 1; b >= 0; --b)
+            if ((e = launch_wpr_list(p, OPEN, kWprMinJ + (uint32_t)b, wl[b], s)) != hipSuccess) return e;
+    }
     // one launch per populated class, largest records first
     KParams q = p;
     for (int c = (int)size_class(max_n); c >= 0; --c) {
         const uint32_t cap = max_n < class_max((uint32_t)c) ? max_n : class_max((uint32_t)c);
         q.lds_rec_bytes = lds_rec_bytes((uint32_t)c, q.ad_len, cap);
-        if ((e = launch_class<OPEN>((uint32_t)c, q, lists + (uint64_t)c * p.count, counts + c,
+        if ((e = launch_class<OPEN>((uint32_t)c, q, lists + (uint64_t)c * p.count, tail + c,
                                     exact ? pop[c] : 0xffffffffu, s)) != hipSuccess)
             return e;
     }
     return hipSuccess;
 }
 
-hipError_t launch_aead(const KParams& p, bool open, uint32_t max_n, bool uniform, uint32_t* lists,
-                       uint32_t* counts, hipStream_t s, uint32_t* over) {
-    return open ? launch_aead_t<true>(p, max_n, uniform, lists, counts, s, over)
-                : launch_aead_t<false>(p, max_n, uniform, lists, counts, s, over);
+hipError_t launch_aead(const KParams& p, bool open, uint32_t max_n, bool uniform, hipStream_t s, uint32_t* over,
+                       hipEvent_t ev_keyed, hipEvent_t ev_start) {
+    return open ? launch_aead_t<true>(p, max_n, uniform, s, over, ev_keyed, ev_start)
+                : launch_aead_t<false>(p, max_n, uniform, s, over, ev_keyed, ev_start);
 }
 
 hipError_t launch_fill(uint8_t* buf, uint64_t stride, uint32_t len, uint32_t count, uint64_t seed,

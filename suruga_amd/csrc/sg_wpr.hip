@@ -68,23 +68,55 @@ constexpr uint32_t kWprChunk = 4096;        // bytes per wave iteration
 constexpr uint32_t kWprLines = 40;          // T digit lines per record
 constexpr uint32_t kWprLineBytes = 48;
 constexpr uint32_t kWprLinesOff = 2 * kWprChunk;  // two chunk buffers, then the T lines
-constexpr uint32_t kWprWaveLds = 2 * kWprChunk + kWprLines * kWprLineBytes + 64;  // 10176: two workgroups per CU
+// after the lines (offsets from the line area): 16 zero bytes read past the
+// last line, the next record's descriptor (bucket launches), the received tag
+constexpr uint32_t kWprDescOff = kWprLines * kWprLineBytes + 16;
+constexpr uint32_t kWprRxOff = kWprDescOff + 48;
+constexpr uint32_t kWprWaveLds = 2 * kWprChunk + kWprRxOff + 16;  // 10192
+// eight waves and the workgroup's next-group slot: two workgroups per CU
+constexpr uint32_t kWprWgLds = kWprWaves * kWprWaveLds + 16;
+static_assert(2 * kWprWgLds <= 160 * 1024, "two workgroups per CU");
+static_assert(kWprDescWords * 4 <= 48, "descriptor slot");
 constexpr uint32_t kWprKeyThreads = 64;
 constexpr uint32_t kWprKeyStride = 81;      // LDS words per record and half
 
-// Geometry of the MAC stream ad || le64(|ad|) || ct || le64(n) for n = 2^14.
+// Geometry of the MAC stream ad || le64(|ad|) || ct || le64(n), n a multiple
+// of 16 (C1: n = 2^14).  A record of n < 2^14 bytes runs right-aligned in the
+// 2^14-byte frame of the kernel (virtual offset 2^14 - n): shifting the
+// ciphertext by a multiple of 16 shifts its MAC block indices and the block
+// count B alike, so every ciphertext byte keeps its weight r^(B - b) 2^(8 k)
+// and the MFMA part of the MAC is the same for every n; only the constant term
+// (AD, length and pad blocks, bias) depends on n.
 struct WprGeom {
-    uint32_t o, sigma, beta, B, rem, delta;
+    uint32_t o, sigma, beta, B, rem, delta, m;
 };
-__device__ __forceinline__ WprGeom wpr_geom(uint32_t adlen) {
+__device__ __forceinline__ WprGeom wpr_geom(uint32_t adlen, uint32_t n) {
     WprGeom g;
     g.o = adlen + 8u;
     g.sigma = g.o & 15u;
     g.beta = g.o >> 4;
-    const uint32_t L = adlen + 16u + kWprN;
+    const uint32_t L = adlen + 16u + n;
     g.B = (L + 15u) >> 4;
     g.rem = L - 16u * (g.B - 1u);
-    g.delta = g.B - g.beta - 1u - 1024u;  // 0 or 1
+    g.m = n >> 4;                        // 16-byte ciphertext chunks
+    g.delta = g.B - g.beta - 1u - g.m;  // 0 or 1
+    return g;
+}
+
+// sum_{i=1..m} x^i and x^m (geo_sum of sg_device.h, also returning the power)
+__device__ __forceinline__ F26 geo_sum_pow(const F26 x, const uint32_t m, F26* pw_out) {
+    F26 g = f26_zero(), pw = f26_one();
+    if (m != 0u) {
+        for (int bit = 31 - __builtin_clz(m); bit >= 0; --bit) {
+            g = mul_add(g, pw.v0, pw.v1, pw.v2, pw.v3, pw.v4, g);
+            pw = fmul(pw, pw);
+            if ((m >> bit) & 1u) {
+                pw = fmul(pw, x);
+                g = f26_add(g, pw);
+            }
+        }
+    }
+    *pw_out = pw;
     return g;
 }
 
@@ -103,33 +135,55 @@ constexpr uint32_t kCJ0 = 0x1bd2d2bu, kCJ1 = 0x36f6f6fu, kCJ2 = 0x3dbdbdbu, kCJ3
 // ---------------------------------------------------------------------------
 // Keying pre-pass: one lane per record, 64 records per wave, the 160-word
 // record (sg_internal.h, kW*) staged in LDS by halves and stored coalesced.
+// LIST: lane = slot of a bucket list (record wl.list[slot], any n of the
+// bucket), which also writes the slot's descriptor; otherwise slot = record
+// and n = 2^14.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void wpr_flush_half(const KParams& p, uint32_t rec0, uint32_t half, const uint32_t* stage,
+__device__ __forceinline__ void wpr_flush_half(const WprList& wl, uint32_t slot0, uint32_t half, const uint32_t* stage,
                                                uint32_t lane) {
-    const uint32_t nrec = p.count - rec0 < kWprKeyThreads ? p.count - rec0 : kWprKeyThreads;
+    const uint32_t nrec = wl.count - slot0 < kWprKeyThreads ? wl.count - slot0 : kWprKeyThreads;
     const uint32_t nvec = nrec * 20u;  // 80 words = 20 x 16 B per record and half
     for (uint32_t v = lane; v < nvec; v += kWprKeyThreads) {
         const uint32_t rr = v / 20u, c = v - rr * 20u;
         const uint32_t* src = stage + rr * kWprKeyStride + 4u * c;
-        st16(p.ws + (uint64_t)(rec0 + rr) * kWprRecWords + 80u * half + 4u * c, u32x4{src[0], src[1], src[2], src[3]});
+        st16(wl.tab + (uint64_t)(slot0 + rr) * kWprRecWords + 80u * half + 4u * c, u32x4{src[0], src[1], src[2], src[3]});
     }
 }
 
-template <bool OPEN>
-__global__ __launch_bounds__(64) void sg_wpr_keying_kernel(const KParams p) {
+// One launch keys every bucket: job b on blocks [blk0[b], blk0[b + 1]).
+struct WprKeyJobs {
+    WprList b[kWprBuckets];
+    uint32_t blk0[kWprBuckets];
+    uint32_t njobs;
+};
+
+template <bool OPEN, bool LIST>
+__global__ __launch_bounds__(64) void sg_wpr_keying_kernel(const KParams p, const WprKeyJobs jobs) {
     __shared__ uint32_t stage[kWprKeyThreads * kWprKeyStride];
     const uint32_t lane = threadIdx.x;
-    const uint32_t rec0 = blockIdx.x * kWprKeyThreads;
-    const uint32_t rec = rec0 + lane;
+    WprList wl = jobs.b[0];
+    uint32_t b0 = 0;
+#pragma unroll
+    for (uint32_t i = 1; i < kWprBuckets; ++i)  // (constant indices: the kernarg table stays in SGPRs)
+        if (i < jobs.njobs && blockIdx.x >= jobs.blk0[i]) {
+            wl = jobs.b[i];
+            b0 = jobs.blk0[i];
+        }
+    const uint32_t slot0 = (blockIdx.x - b0) * kWprKeyThreads;
+    const uint32_t slot = slot0 + lane;
     uint32_t* st = stage + lane * kWprKeyStride;
     const uint32_t adlen = p.tls ? 13u : p.ad_len;
-    const WprGeom G = wpr_geom(adlen);
-    if (blockIdx.x == 0u && lane == 0u) p.ws[(uint64_t)p.count * kWprRecWords] = 0u;  // the AEAD kernel's group counter
+    if (blockIdx.x == b0 && lane == 0u) *wl.ctr = 0u;  // the record kernel's group counter
+
+    const bool act = slot < wl.count;
+    const uint32_t rec = LIST ? (act ? wl.list[slot] : 0u) : slot;
+    uint32_t n = kWprN;
+    if constexpr (LIST) n = act ? p.len[rec] - (OPEN ? 16u : 0u) : kWprN;
+    const WprGeom G = wpr_geom(adlen, n);
 
     F26 r = f26_zero();
     uint32_t s[4] = {0u, 0u, 0u, 0u};
     RecKey rk = {};
-    const bool act = rec < p.count;
     if (act) {
         rk = record_key(p, rec);
         uint32_t ks[16];
@@ -137,6 +191,15 @@ __global__ __launch_bounds__(64) void sg_wpr_keying_kernel(const KParams p) {
         // r = clamp(pk[0..16]) (poly1305.rs:197-203), s = pk[16..32] (chacha20_poly1305.rs:32-39)
         r = words_to_f26(ks[0] & 0x0fffffffu, ks[1] & 0x0ffffffcu, ks[2] & 0x0ffffffcu, ks[3] & 0x0ffffffcu, 0u);
         s[0] = ks[4]; s[1] = ks[5]; s[2] = ks[6]; s[3] = ks[7];
+        if constexpr (LIST) {  // the slot's descriptor: where the record lives, its length and nonce
+            const uint64_t io = p.in_off ? p.in_off[rec] : p.in_stride * rec;
+            const uint64_t oo = p.out_off ? p.out_off[rec] : p.out_stride * rec;
+            const uint32_t ki = p.key_index ? p.key_index[rec] : 0u;
+            uint32_t* d = wl.desc + (uint64_t)slot * kWprDescWords;
+            st16(d, u32x4{(uint32_t)io, (uint32_t)(io >> 32), (uint32_t)oo, (uint32_t)(oo >> 32)});
+            st16(d + 4, u32x4{n, rec, ki, rk.n14});
+            st16(d + 8, u32x4{rk.n15, 0u, 0u, 0u});
+        }
     }
 
     // ---- second half: lo[b] = R^b, hi[h][a] = 2^(32 h) R^(8 a) (R = r^4) ----
@@ -159,7 +222,7 @@ __global__ __launch_bounds__(64) void sg_wpr_keying_kernel(const KParams p) {
     }
     const F26 T = y;  // R^32 = r^128
     __syncthreads();
-    wpr_flush_half(p, rec0, 1u, stage, lane);
+    wpr_flush_half(wl, slot0, 1u, stage, lane);
     __syncthreads();
 
     // ---- first half: s, ctot, rd[u] = r^(1 + delta + u), tk[k] = T^k ----
@@ -178,15 +241,21 @@ __global__ __launch_bounds__(64) void sg_wpr_keying_kernel(const KParams p) {
         sum_t = f26_add(sum_t, t);
         t = fmul(t, T);
     }
-    const F26 T8 = t;  // r^1024
 
-    // geometric sums: SW = sum_{u<32} R^u, g = G(1024) = (r + r^2 + r^3 + r^4) SW sum_k T^k
+    // geometric sums: SW = sum_{u<32} R^u; g = G(m) = sum_{i=1..m} r^i and rm = r^m
+    // (m = n / 16: for n = 2^14, G(1024) = (r + r^2 + r^3 + r^4) SW sum_k T^k, r^1024 = T^8)
     const F26 SW = fmul(carry1(sum_hi), carry1(sum_lo));
-    const F26 G4 = carry1(f26_add(f26_add(r, r2), f26_add(r3, R)));
-    const F26 g = fmul(fmul(G4, SW), carry1(sum_t));
+    F26 g, rm;
+    if constexpr (LIST) {
+        g = geo_sum_pow(r, G.m, &rm);
+    } else {
+        const F26 G4 = carry1(f26_add(f26_add(r, r2), f26_add(r3, R)));
+        g = fmul(fmul(G4, SW), carry1(sum_t));
+        rm = t;
+    }
     // pads (poly1305.rs:224-225): 2^128 sum_{b < B-1} r^(B-b) + 2^(8 rem) r
-    //   = 2^128 G(B) + (2^(8 rem) + p - 2^128) r,  G(B) = G(1024) + r^1024 G(B - 1024)
-    const F26 GB = fmul_add(T8, geo_sum(r, G.B - 1024u), g);
+    //   = 2^128 G(B) + (2^(8 rem) + p - 2^128) r,  G(B) = G(m) + r^m G(B - m)
+    const F26 GB = fmul_add(rm, geo_sum(r, G.B - G.m), g);
     F26 pads = mul_add(GB, 0u, 0u, 0u, 0u, 1u << 24, f26_zero());
     {
         F26 cf = F26{0x3fffffbu, 0x3ffffffu, 0x3ffffffu, 0x3ffffffu, 0x2ffffffu};  // p - 2^128
@@ -199,40 +268,40 @@ __global__ __launch_bounds__(64) void sg_wpr_keying_kernel(const KParams p) {
         pads = fmul_add(cf, r, pads);
     }
     // i8 bias: 128 sum over the ciphertext bytes of their weights
-    //   = r^delta G(1024) (A1 r + A2),  A1 = sum_{k=sigma}^{15} 128 2^(8k),  A2 = sum_{k<sigma} 128 2^(8k)
+    //   = r^delta G(m) (A1 r + A2),  A1 = sum_{k=sigma}^{15} 128 2^(8k),  A2 = sum_{k<sigma} 128 2^(8k)
     F26 bias;
     {
         uint32_t a1[4], a2[4];
 #pragma unroll
         for (uint32_t w = 0; w < 4; ++w) {
-            const uint32_t m = bytes_from(w, G.sigma);
-            a1[w] = 0x80808080u & m;
-            a2[w] = 0x80808080u & ~m;
+            const uint32_t mk = bytes_from(w, G.sigma);
+            a1[w] = 0x80808080u & mk;
+            a2[w] = 0x80808080u & ~mk;
         }
         const F26 A1 = words_to_f26(a1[0], a1[1], a1[2], a1[3], 0u);
         const F26 A2 = words_to_f26(a2[0], a2[1], a2[2], a2[3], 0u);
         bias = fmul(fmul(g, fmul_add(A1, r, A2)), rdel);
     }
-    // accumulator seed: -(2^24 sum_c 2^(8c)) SW
+    // accumulator seed: -(2^24 sum_c 2^(8c)) SW (every column, the idle lanes' too)
     const F26 seed = mul_add(SW, kCJ0, kCJ1, kCJ2, kCJ3, kCJ4, f26_zero());
-    // prefix ad || le64(|ad|) (stream bytes < o) as blocks 0..beta: Horner, then r^(B - beta) = r^1024 r^(1 + delta)
+    // prefix ad || le64(|ad|) (stream bytes < o) as blocks 0..beta: Horner, then r^(B - beta) = r^m r^(1 + delta)
     F26 hp = f26_zero();
     if (act) {
         for (uint32_t b = 0; b <= G.beta; ++b) {
             uint32_t w[4] = {0u, 0u, 0u, 0u};
             for (uint32_t i = 0; i < 16u; ++i) {
                 const uint32_t pos = 16u * b + i;
-                if (pos < G.o) w[i >> 2] |= (uint32_t)prefix_byte(p, rec, rk.seq, kWprN, adlen, pos) << (8u * (i & 3u));
+                if (pos < G.o) w[i >> 2] |= (uint32_t)prefix_byte(p, rec, rk.seq, n, adlen, pos) << (8u * (i & 3u));
             }
             hp = fmul_add(hp, r, words_to_f26(w[0], w[1], w[2], w[3], 0u));
         }
     }
-    const F26 prefix = fmul(fmul(hp, T8), rd0);
-    // suffix le64(n) at stream offset o + n = 16 (beta + 1024) + sigma: n 2^(8 sigma) split at 2^128
+    const F26 prefix = fmul(fmul(hp, rm), rd0);
+    // suffix le64(n) at stream offset o + n = 16 (beta + m) + sigma: n 2^(8 sigma) split at 2^128
     F26 suffix;
     {
         const uint32_t wi = G.sigma >> 2, bs = 8u * (G.sigma & 3u);
-        const uint64_t v = (uint64_t)kWprN << bs;
+        const uint64_t v = (uint64_t)n << bs;
         uint32_t w[5] = {0u, 0u, 0u, 0u, 0u};
 #pragma unroll
         for (uint32_t i = 0; i < 4; ++i) {
@@ -246,7 +315,7 @@ __global__ __launch_bounds__(64) void sg_wpr_keying_kernel(const KParams p) {
     const F26 ctot = carry1(f26_add(f26_add(f26_add(pads, bias), f26_add(seed, prefix)), suffix));
     store_f26(st + kWCtot, ctot);
     __syncthreads();
-    wpr_flush_half(p, rec0, 0u, stage, lane);
+    wpr_flush_half(wl, slot0, 0u, stage, lane);
 }
 
 // ---------------------------------------------------------------------------
@@ -357,14 +426,28 @@ __device__ __forceinline__ void dma_one(uint32_t l0, const void* g) {
                  : "memory");
 }
 
-template <bool OPEN, bool TLS>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) void sg_wpr_kernel(const KParams p) {
+// Where a record lives and what keys it (uniform per wave).  Uniform batches
+// derive it from the record index; bucket launches read the slot's descriptor.
+struct RecDesc {
+    uint64_t io, oo;    // byte offsets of the input / output record
+    uint32_t n;         // plaintext length
+    uint32_t rec;       // record index (status, key index, sequence number)
+    uint32_t ki, n14, n15;
+};
+
+template <bool OPEN, bool TLS, uint32_t J, bool LIST>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) void sg_wpr_kernel(const KParams p,
+                                                                                               const WprList wl) {
+    static_assert(J >= 1u && J <= 4u && (LIST || J == 4u), "uniform launches are full 16 KiB records");
+    constexpr uint32_t j0 = 4u - J;  // the first chunk of the right-aligned record in the 16 KiB frame
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const uint32_t wave = uniform(threadIdx.x >> 6), lane = threadIdx.x & 63u;
     uint8_t* buf = lds + wave * kWprWaveLds;
     uint8_t* lines = buf + kWprLinesOff;  // also the landing area of the record's keying table
     const uint32_t lds_wave = uniform((uint32_t)(uintptr_t)buf);
     const uint32_t lds_lines = uniform(lds_wave + kWprLinesOff);
+    const uint32_t lds_desc = uniform(lds_lines + kWprDescOff);
+    const uint32_t lds_rxs = uniform(lds_lines + kWprRxOff);
     const uint32_t hh = lane >> 5, q = lane & 31u;
     const uint32_t adlen = TLS ? 13u : p.ad_len;
     const uint32_t sigma = (adlen + 8u) & 15u;
@@ -377,39 +460,108 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     // the lane's MAC window base (line 5 (1 - hh), dword of byte 47 - q) and shift
     const uint8_t* mac_base = lines + 240u * (1u - hh) + 4u * ((47u - q) >> 2);
     const uint32_t mac_shift = (47u - q) & 3u;
-    const uint32_t ngroups = (p.count + kWprWaves - 1u) / kWprWaves;
+    const uint32_t cnt = wl.count;
+    const uint32_t ngroups = (cnt + kWprWaves - 1u) / kWprWaves;
 
-    // Chunk c of a record is fetched by LDS-DMA into buffer c & 1, one chunk
-    // ahead: lane l of DMA instruction k lands at LDS unit 64 k + l and reads
-    // global unit 64 k + wunit(l), so LDS unit phi(g) holds global unit g
-    // (phi = wunit within each 64-unit piece, an involution).  The record's
-    // keying table (640 B) is fetched into the line area the same way.  The
-    // only vector-memory operations of the kernel are these DMAs and the
-    // output stores, so the waits below count exactly.
-    auto dma_chunk_of = [&](uint32_t rec, uint32_t c) {
-        dma_chunk(lds_wave + kWprChunk * (c & 1u), p.in + p.in_stride * rec + kWprChunk * c + 16u * wunit);
+    // The record of slot `slot` (slot < cnt): uniform batches from the strides,
+    // bucket launches from the descriptor the keying kernel wrote.
+    auto desc_of_slot = [&](uint32_t slot) {
+        RecDesc d;
+        if constexpr (LIST) {
+            const uint32_t* dw = wl.desc + (uint64_t)slot * kWprDescWords;
+            d.io = (uint64_t)cload(dw, 0) | ((uint64_t)cload(dw, 1) << 32);
+            d.oo = (uint64_t)cload(dw, 2) | ((uint64_t)cload(dw, 3) << 32);
+            d.n = cload(dw, 4);
+            d.rec = cload(dw, 5);
+            d.ki = cload(dw, 6);
+            d.n14 = cload(dw, 7);
+            d.n15 = cload(dw, 8);
+        } else {
+            d.rec = slot;
+            d.io = p.in_stride * slot;
+            d.oo = p.out_stride * slot;
+            d.n = kWprN;
+            d.ki = p.key_index ? cload(p.key_index, slot) : 0u;
+            // nonce (chacha20.rs:25-51; TLS: be64(seq), tls.rs:103)
+            if constexpr (TLS) {
+                uint64_t seq = p.seq0 + slot;
+                if (p.seq) seq = (uint64_t)cload(p.seq, 2ull * slot) | ((uint64_t)cload(p.seq, 2ull * slot + 1u) << 32);
+                d.n14 = bswap32((uint32_t)(seq >> 32));
+                d.n15 = bswap32((uint32_t)seq);
+            } else {
+                d.n14 = cload(p.nonces, 2ull * slot);
+                d.n15 = cload(p.nonces, 2ull * slot + 1u);
+            }
+        }
+        return d;
     };
-    auto dma_table_of = [&](uint32_t rec) {  // into the line area
-        if (lane < kWprRecWords / 4u) dma_one(lds_lines, p.ws + (uint64_t)rec * kWprRecWords + 4u * lane);
+    // the next record's descriptor, landed in the wave's LDS descriptor slot
+    auto desc_from_lds = [&]() {
+        const uint32_t* dl = reinterpret_cast<const uint32_t*>(lines + kWprDescOff);
+        RecDesc d;
+        d.io = (uint64_t)uniform(dl[0]) | ((uint64_t)uniform(dl[1]) << 32);
+        d.oo = (uint64_t)uniform(dl[2]) | ((uint64_t)uniform(dl[3]) << 32);
+        d.n = uniform(dl[4]);
+        d.rec = uniform(dl[5]);
+        d.ki = uniform(dl[6]);
+        d.n14 = uniform(dl[7]);
+        d.n15 = uniform(dl[8]);
+        return d;
     };
-    // Record groups are handed out dynamically: the first one is the
-    // workgroup's index, every later one comes from a device counter (zeroed by
-    // the keying kernel), fetched by wave 0 at the start of the previous group
-    // and passed to the other waves through LDS.  The two workgroups sharing a
-    // CU do not progress at the same rate (a static g += gridDim.x split left
-    // the fastest waves idle for the last 40 % of the launch).
-    uint32_t* const ctr = p.ws + (uint64_t)p.count * kWprRecWords;
-    uint32_t* const gslot = reinterpret_cast<uint32_t*>(lds + kWprLinesOff + kWprLines * kWprLineBytes + 32u);
+
+    // Chunk c of a record is fetched by LDS-DMA into the wave buffer that the
+    // previous chunk does not occupy, one chunk ahead: lane l of DMA piece k
+    // lands at LDS unit 64 k + l and reads global unit 64 k + wunit(l), so LDS
+    // unit phi(g) holds global unit g (phi = wunit within each 64-unit piece,
+    // an involution).  The record sits right-aligned in the 16 KiB frame:
+    // frame byte v is record byte v - vs (vs = 2^14 - n), so the first chunk
+    // j0 of a shorter record starts with lo = 4096 J - n bytes that belong to
+    // no record; their lanes neither load nor store.  The record's keying
+    // table (640 B) is fetched into the line area the same way.  The only
+    // vector-memory operations of the kernel are these DMAs, the descriptor
+    // DMA and the output stores, so the waits below count exactly.
+    auto dma_piece_of = [&](uint32_t ldsb, const uint8_t* chunk_base, uint32_t k, uint32_t lo) {
+        // chunk_base: the record's frame chunk start in real addresses (may lie before the record)
+        if (!LIST || 1024u * k + 16u * wunit >= lo) dma_sv(uniform(ldsb + 1024u * k), chunk_base + 1024u * k, 16u * wunit);
+    };
+    auto dma_table_of = [&](uint32_t slot) {  // into the line area
+        if (lane < kWprRecWords / 4u) dma_one(lds_lines, wl.tab + (uint64_t)slot * kWprRecWords + 4u * lane);
+    };
+    auto dma_desc_of = [&](uint32_t slot) {  // LIST: into the descriptor slot
+        if (lane < kWprDescWords / 4u) dma_one(lds_desc, wl.desc + (uint64_t)slot * kWprDescWords + 4u * lane);
+    };
+    // Record groups are handed out dynamically: the first ones are static, every
+    // later one comes from a device counter (zeroed by the keying kernel),
+    // fetched by wave 0 during a group and passed to the other waves through
+    // LDS.  The two workgroups sharing a CU do not progress at the same rate (a
+    // static g += gridDim.x split left the fastest waves idle for the last 40 %
+    // of the launch).  Uniform launches fetch one group ahead (the next
+    // record's first chunk is addressed from its index); bucket launches two
+    // groups ahead, so that the next record's descriptor can be fetched a whole
+    // record before its first chunk.
+    uint32_t* const ctr = wl.ctr;
+    uint32_t* const gslot = reinterpret_cast<uint32_t*>(lds + kWprWaves * kWprWaveLds);
     uint32_t g = blockIdx.x;
-    if (g < ngroups && g * kWprWaves + wave < p.count) {
-        dma_chunk_of(g * kWprWaves + wave, 0u);
-        dma_table_of(g * kWprWaves + wave);
+    uint32_t gnx = LIST ? blockIdx.x + gridDim.x : ngroups;  // LIST: the next group, known a record ahead
+    constexpr uint32_t kStatic = LIST ? 2u : 1u;            // groups handed out statically per workgroup
+    RecDesc cd = {};                                        // the current record
+    uint32_t par = 0u;  // LIST, J odd: the buffer of the record's first chunk alternates
+    if (g < ngroups && g * kWprWaves + wave < cnt) {
+        const uint32_t slot = g * kWprWaves + wave;
+        cd = desc_of_slot(slot);
+        const uint32_t vs = kWprN - cd.n, lo = kWprChunk * J - cd.n;
+        const uint8_t* cb0 = p.in + cd.io + kWprChunk * j0 - vs;
+#pragma unroll
+        for (uint32_t k = 0; k < 4u; ++k) dma_piece_of(lds_wave, cb0, k, lo);
+        dma_table_of(slot);
     }
     bool first = true;
     // the previous chunk's output waits in its LDS buffer and leaves during
     // the next chunk's first double rounds (pend: it belongs to an active record)
     bool pend = false;
     uint8_t* pend_dst = p.out;
+    uint32_t pend_lo = 0u;  // bytes of the pending chunk before the record (LIST: the first chunk)
+    uint32_t lastb = 0u;    // the buffer of the last chunk
 
 #if SG_WPR_PROFILE
     uint64_t prof[kProfPhases] = {};
@@ -423,29 +575,24 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
 #if SG_WPR_PROFILE
         prof[6] += 1;  // records (groups) this wave ran
 #endif
-        const uint32_t rec = g * kWprWaves + wave;
-        const bool active = rec < p.count;  // an inactive wave still runs every round and barrier
-        const uint32_t recl = rec < p.count ? rec : p.count - 1u;
-        uint32_t gn = ngroups, nrec = 0u;  // the next group: known from iteration 3 on
+        const uint32_t slot = g * kWprWaves + wave;
+        const bool active = slot < cnt;  // an inactive wave still runs every round and barrier
+        // (an inactive wave takes any record: its results are not stored)
+        if constexpr (!LIST) cd = desc_of_slot(active ? slot : cnt - 1u);
+        else if (!active) cd = desc_of_slot(cnt - 1u);
+        const uint32_t n = LIST ? cd.n : kWprN;
+        const uint32_t vs = kWprN - n;                             // frame offset of the record
+        const uint32_t lo = LIST ? kWprChunk * J - n : 0u;         // idle bytes of chunk j0
+        const uint8_t* inb = p.in + cd.io;
+        uint8_t* outb = p.out + cd.oo;
+        uint32_t gn = ngroups, gnn = ngroups;  // the next group (uniform launches: known from iteration 3 on)
+        if constexpr (LIST) gn = gnx;
+        RecDesc nd = {};                       // the next record (LIST: from iteration j0 + 1 on)
         bool next = false;
-        uint8_t* out = p.out + p.out_stride * recl;
-        // key, nonce (chacha20.rs:25-51; TLS: be64(seq), tls.rs:103), received tag
         uint32_t kw[8];
-        {
-            const uint32_t ki = p.key_index ? cload(p.key_index, recl) : 0u;
 #pragma unroll
-            for (uint32_t i = 0; i < 8u; ++i) kw[i] = cload(p.keys, 8ull * ki + i);
-        }
-        uint32_t n14, n15;
-        if constexpr (TLS) {
-            uint64_t seq = p.seq0 + recl;
-            if (p.seq) seq = (uint64_t)cload(p.seq, 2ull * recl) | ((uint64_t)cload(p.seq, 2ull * recl + 1u) << 32);
-            n14 = bswap32((uint32_t)(seq >> 32));
-            n15 = bswap32((uint32_t)seq);
-        } else {
-            n14 = cload(p.nonces, 2ull * recl);
-            n15 = cload(p.nonces, 2ull * recl + 1u);
-        }
+        for (uint32_t i = 0; i < 8u; ++i) kw[i] = cload(p.keys, 8ull * cd.ki + i);
+        const uint32_t n14 = cd.n14, n15 = cd.n15;
         // The column quarter rounds 1-3 of the first double round see no block
         // counter (word 13 is 0, chacha20.rs:114-121): the same for every lane
         // and chunk of the record, so they run once per record on the SALU.
@@ -456,11 +603,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
         // (tools/gen_chacha_grp.py, SG_CHACHA_DR1S_*; tests/test_chacha_asm_model.py)
         const uint32_t S0 = u[0] + u[4], T1 = u[1] + u[6], T2 = u[2] + u[7];
         const uint32_t T13 = rotl32(u[13] ^ T2, 16);
-        uint32_t rx[4] = {0u, 0u, 0u, 0u};
-        if constexpr (OPEN) {  // the received tag (chacha20_poly1305.rs:72-73)
-            const uint8_t* tg = p.in + p.in_stride * recl + kWprN;
-            rx[0] = cload(tg, 0); rx[1] = cload(tg, 1); rx[2] = cload(tg, 2); rx[3] = cload(tg, 3);
-        }
 
         // ---- the keying table has landed (it was followed only by the previous
         // record's tag / status store; the chunk-0 DMA is older)
@@ -471,6 +613,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
         uint32_t fetched = 0u;
         if (wave == 0u && lane == 0u)
             fetched = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if constexpr (LIST) {  // the next record's descriptor, a record ahead of its first chunk
+            if (gn < ngroups && gn * kWprWaves + wave < cnt) dma_desc_of(gn * kWprWaves + wave);
+        }
+        // open: the received tag (chacha20_poly1305.rs:72-73) into the wave's tag
+        // slot by LDS-DMA; it is read in the epilogue (a scalar load here would
+        // hold up the table reads below until it returned)
+        if (OPEN && lane == 0u) dma_one(lds_rxs, inb + n);
         SG_TICK(t_tw);
         SG_ACC(0, t_rs, t_tw);  // wait for the keying table
         const uint32_t* tab = reinterpret_cast<const uint32_t*>(lines);
@@ -485,8 +634,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
         // 17 signed base-256 digits, digit i at byte 47 - sigma - i, zeros elsewhere
         F26 lv = f26_zero();
         if (lane < kWprLines) {
-            const uint32_t k = lane / 5u, u = lane - 5u * k;
-            lv = fmul(load_f26(tab + kWRd + 5u * u), load_f26(tab + kWTk + 5u * k));
+            const uint32_t k = lane / 5u, uu = lane - 5u * k;
+            lv = fmul(load_f26(tab + kWRd + 5u * uu), load_f26(tab + kWTk + 5u * k));
         }
         wave_lds_sync();  // every table read is done before the lines overwrite it
         if (lane < kWprLines) {
@@ -587,25 +736,35 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
 #define SG_PIN() __builtin_amdgcn_sched_barrier(0)
 
 #pragma unroll
-        for (uint32_t j = 0; j < 4u; ++j) {
+        for (uint32_t j = j0; j < 4u; ++j) {
             SG_TICK(t_js);
-            // chunk j has landed in buffer j & 1 (j >= 1: its DMA was the last
-            // memory operation of iteration j - 1; j = 0: waited for with the table)
-            if (j > 0u) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (j == 1u && wave == 0u && lane == 0u) *gslot = gridDim.x + fetched;  // the atomic has returned
+            // chunk j has landed (j > j0: its DMA was the last memory operation
+            // of iteration j - 1; j = j0: waited for with the table), and so has
+            // the next record's descriptor (LIST)
+            if (j > j0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (j == j0 + 1u && wave == 0u && lane == 0u) *gslot = kStatic * gridDim.x + fetched;  // the atomic has returned
             wave_lds_sync();
-            if (j == 3u) {  // wave 0 published it before the barriers of iterations 1 and 2
+            if constexpr (LIST) {
+                if (j == j0 + 1u && gn < ngroups && gn * kWprWaves + wave < cnt) {
+                    nd = desc_from_lds();
+                    next = true;
+                }
+            } else if (j == 3u) {  // wave 0 published it before the barriers of iterations 1 and 2
                 gn = uniform(*gslot);
-                nrec = gn * kWprWaves + wave;
-                next = gn < ngroups && nrec < p.count;
+                next = gn < ngroups && gn * kWprWaves + wave < cnt;
+                nd.io = p.in_stride * (gn * kWprWaves + wave);  // only the address: the rest at its start
             }
             SG_TICK(t_jw);
             SG_ACC(2, t_js, t_jw);  // wait for the chunk
-            uint8_t* cb = buf + kWprChunk * (j & 1u);
-            uint8_t* pb = buf + kWprChunk * ((j + 1u) & 1u);  // the pending output
+            // buffers: chunk j in bj, the pending output in the other one
+            const uint32_t bj = ((j - j0) + par) & 1u;
+            uint8_t* cb = buf + kWprChunk * bj;
+            uint8_t* pb = buf + kWprChunk * (bj ^ 1u);
+            const uint32_t plo = pend_lo;
 
-            // keystream block 64 j + lane + 1 (chacha20_poly1305.rs:52), lock-step rounds
-            const uint32_t ctr = 64u * j + lane + 1u;
+            // keystream block 64 j + lane + 1 of the frame = block 64 j + lane + 1 - vs / 64 of the
+            // record (chacha20_poly1305.rs:52), lock-step rounds
+            const uint32_t ctr = 64u * j + lane + 1u - (vs >> 6);
             uint32_t x[16];
             x[12] = ctr;
             u32x4 D[4];
@@ -626,23 +785,28 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
             // (the same LDS range): the stores and DMAs of the 16 waves of a CU
             // spread over five gaps instead of queueing behind each other.
             auto out_piece = [&](uint32_t k) { return ld16(pb + 1024u * k + 16u * wunit); };
-            auto store_piece = [&](uint32_t k, const u32x4& v) { st16(pend_dst + 1024u * k + 16u * lane, v); };
+            auto store_piece = [&](uint32_t k, const u32x4& v) {
+                if (!LIST || 1024u * k + 16u * lane >= plo) st16(pend_dst + 1024u * k + 16u * lane, v);
+            };
             auto dma_piece = [&](uint32_t k) {
+                const uint32_t ldsb = lds_wave + kWprChunk * (bj ^ 1u);
                 if (j < 3u) {
-                    if (active)
-                        dma_sv(uniform(lds_wave + kWprChunk * ((j + 1u) & 1u) + 1024u * k),
-                               p.in + p.in_stride * rec + kWprChunk * (j + 1u) + 1024u * k, 16u * wunit);
+                    if (active) dma_piece_of(ldsb, inb + kWprChunk * (j + 1u) - vs, k, 0u);
                 } else if (next) {
-                    dma_sv(uniform(lds_wave + 1024u * k), p.in + p.in_stride * nrec + 1024u * k, 16u * wunit);
+                    const uint32_t nvs = kWprN - (LIST ? nd.n : kWprN);
+                    dma_piece_of(ldsb, p.in + nd.io + kWprChunk * j0 - nvs, k, LIST ? kWprChunk * J - nd.n : 0u);
                 }
             };
             u32x4 oa = {}, ob = {};
-            if (j > 0u) mac_load(j - 1u, 0u, R0);
+            if (j > j0) mac_load(j - 1u, 0u, R0);
             if (pend) oa = out_piece(0u);
             SG_PIN();
             SG_DR();
             SG_PIN();
-            if (j > 0u) {
+            if (LIST && j == 3u) {  // wave 0 published it at the start of iteration j0 + 1 (LIST: J >= 2)
+                gnn = uniform(*gslot);
+            }
+            if (j > j0) {
                 mac_mfma(R0, A[0]);
                 mac_load(j - 1u, 1u, R1);
             }
@@ -653,7 +817,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
             SG_PIN();
             SG_DR();
             SG_PIN();
-            if (j > 0u) {
+            if (j > j0) {
                 mac_mfma(R1, A[1]);
                 mac_load(j - 1u, 2u, R0);
             }
@@ -665,7 +829,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
             SG_PIN();
             SG_DR();
             SG_PIN();
-            if (j > 0u) {
+            if (j > j0) {
                 mac_mfma(R0, A[2]);
                 mac_load(j - 1u, 3u, R1);
             }
@@ -677,7 +841,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
             SG_PIN();
             SG_DR();
             SG_PIN();
-            if (j > 0u) mac_mfma(R1, A[3]);
+            if (j > j0) mac_mfma(R1, A[3]);
             if (pend) store_piece(3u, ob);
             dma_piece(2u);
             SG_PIN();
@@ -716,7 +880,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
             SG_ACC(3, t_jw, t_jr);  // rounds (+ MAC of the previous chunk)
             if (j == 3u && next) {  // the line area is read out: the next record's table lands there
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                dma_table_of(nrec);
+                dma_table_of(gn * kWprWaves + wave);
             }
             // feed-forward (chacha20.rs:104-106) and XOR (chacha20.rs:143-153)
             u32x4 O[4];
@@ -724,9 +888,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
             O[1] = D[1] ^ u32x4{x[4] + kw[0], x[5] + kw[1], x[6] + kw[2], x[7] + kw[3]};
             O[2] = D[2] ^ u32x4{x[8] + kw[4], x[9] + kw[5], x[10] + kw[6], x[11] + kw[7]};
             O[3] = D[3] ^ u32x4{x[12] + ctr, x[13], x[14] + n14, x[15] + n15};
-            // the MAC reads the ciphertext: received (open) or just produced (seal)
+            // the MAC reads the ciphertext: received (open) or just produced (seal);
+            // the lanes of the frame before the record contribute nothing (i8 0)
 #pragma unroll
             for (uint32_t i = 0; i < 4u; ++i) A[i] = OPEN ? D[i] : O[i];
+            if (LIST && j == j0 && 64u * lane < lo) {
+#pragma unroll
+                for (uint32_t i = 0; i < 4u; ++i) A[i] = u32x4{0x80808080u, 0x80808080u, 0x80808080u, 0x80808080u};
+            }
             if (j == 3u) {
                 SG_PIN();
 #pragma unroll
@@ -739,7 +908,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
 #pragma unroll
             for (uint32_t i = 0; i < 4u; ++i) st16(cb + 16u * (4u * lane + (i ^ xq)), O[i]);
             pend = active;
-            pend_dst = out + kWprChunk * j;
+            pend_dst = outb + kWprChunk * j - vs;
+            pend_lo = j == j0 ? lo : 0u;
+            lastb = bj;
             SG_TICK(t_je);
             SG_ACC(4, t_jr, t_je);  // feed-forward, XOR, staging, stores
 #if SG_WPR_PROFILE
@@ -779,20 +950,28 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
         tag_words(fs, sk, tw);
         if (active && lane == 0u) {
             if constexpr (!OPEN) {
-                st16(out + kWprN, u32x4{tw[0], tw[1], tw[2], tw[3]});  // ct || tag (chacha20_poly1305.rs:55)
+                st16(outb + n, u32x4{tw[0], tw[1], tw[2], tw[3]});  // ct || tag (chacha20_poly1305.rs:55)
             } else {
                 // constant-time compare: diff |= a ^ b over all 16 bytes (chacha20_poly1305.rs:84-87)
-                const uint32_t diff = (rx[0] ^ tw[0]) | (rx[1] ^ tw[1]) | (rx[2] ^ tw[2]) | (rx[3] ^ tw[3]);
-                p.status[rec] = diff != 0u ? 1u : 0u;
+                const uint32_t* rxl = reinterpret_cast<const uint32_t*>(lines + kWprRxOff);
+                const uint32_t diff = (rxl[0] ^ tw[0]) | (rxl[1] ^ tw[1]) | (rxl[2] ^ tw[2]) | (rxl[3] ^ tw[3]);
+                p.status[cd.rec] = diff != 0u ? 1u : 0u;
             }
         }
         g = gn;
+        if constexpr (LIST) {
+            gnx = gnn;
+            par ^= J & 1u;
+        }
+        if constexpr (LIST) cd = nd;
     }
     if (pend) {  // the last record's last chunk
         wave_lds_sync();
-        const uint8_t* pb = buf + kWprChunk;
+        const uint8_t* pb = buf + kWprChunk * lastb;
 #pragma unroll
-        for (uint32_t k = 0; k < 4u; ++k) st16(pend_dst + 1024u * k + 16u * lane, ld16(pb + 1024u * k + 16u * wunit));
+        for (uint32_t k = 0; k < 4u; ++k)
+            if (!LIST || 1024u * k + 16u * lane >= pend_lo)
+                st16(pend_dst + 1024u * k + 16u * lane, ld16(pb + 1024u * k + 16u * wunit));
     }
 #if SG_WPR_PROFILE
     SG_TICK(t_end);
@@ -825,32 +1004,88 @@ extern "C" int sg_wpr_profile_read(unsigned long long* host, size_t n) {
 namespace sg {
 #endif
 
+static hipError_t device_cus(int* cus) {
+    int dev = 0;
+    hipError_t e;
+    if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
+    *cus = dev >= 0 && dev < 64 ? __atomic_load_n(&g_cus[dev], __ATOMIC_RELAXED) : 0;
+    if (*cus <= 0) {
+        if ((e = hipDeviceGetAttribute(cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return e;
+        if (dev >= 0 && dev < 64) __atomic_store_n(&g_cus[dev], *cus, __ATOMIC_RELAXED);
+    }
+    return hipSuccess;
+}
+
+// persistent grid: two workgroups (16 waves) per CU, at most one per record group
+static uint32_t wpr_grid(int cus, uint32_t count) {
+    const uint32_t ngroups = (count + kWprWaves - 1u) / kWprWaves;
+    const uint32_t grid = 2u * (uint32_t)cus;
+    return grid < ngroups ? grid : ngroups;
+}
+
 hipError_t launch_wpr(const KParams& p, bool open, hipStream_t s, hipEvent_t ev_keyed, hipEvent_t ev_start) {
+    WprList wl;
+    wl.list = nullptr;
+    wl.count = p.count;
+    wl.tab = p.ws + (uint64_t)p.count * kWsWprTab;
+    wl.desc = nullptr;
+    wl.ctr = ws_tail(p.ws, p.count) + kTailCtr + kWprBuckets;
+    WprKeyJobs jobs = {};
+    jobs.b[0] = wl;
+    jobs.njobs = 1;
     const uint32_t kgrid = (p.count + kWprKeyThreads - 1u) / kWprKeyThreads;
     if (open)
-        hipLaunchKernelGGL((sg_wpr_keying_kernel<true>), dim3(kgrid), dim3(kWprKeyThreads), 0, s, p);
+        hipLaunchKernelGGL((sg_wpr_keying_kernel<true, false>), dim3(kgrid), dim3(kWprKeyThreads), 0, s, p, jobs);
     else
-        hipLaunchKernelGGL((sg_wpr_keying_kernel<false>), dim3(kgrid), dim3(kWprKeyThreads), 0, s, p);
+        hipLaunchKernelGGL((sg_wpr_keying_kernel<false, false>), dim3(kgrid), dim3(kWprKeyThreads), 0, s, p, jobs);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (ev_keyed && (e = hipEventRecord(ev_keyed, s)) != hipSuccess) return e;
     if (ev_start && (e = hipEventRecord(ev_start, s)) != hipSuccess) return e;
-    int dev = 0;
-    if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
-    int cus = dev >= 0 && dev < 64 ? __atomic_load_n(&g_cus[dev], __ATOMIC_RELAXED) : 0;
-    if (cus <= 0) {
-        if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return e;
-        if (dev >= 0 && dev < 64) __atomic_store_n(&g_cus[dev], cus, __ATOMIC_RELAXED);
-    }
-    const uint32_t ngroups = (p.count + kWprWaves - 1u) / kWprWaves;
-    uint32_t grid = 2u * (uint32_t)cus;  // two workgroups (16 waves) per CU
-    if (grid > ngroups) grid = ngroups;
-    const size_t lds = kWprWaves * kWprWaveLds;
-#define SG_WPR_LAUNCH(O, T) hipLaunchKernelGGL((sg_wpr_kernel<O, T>), dim3(grid), dim3(512), lds, s, p)
+    int cus = 0;
+    if ((e = device_cus(&cus)) != hipSuccess) return e;
+    const uint32_t grid = wpr_grid(cus, p.count);
+#define SG_WPR_LAUNCH(O, T) hipLaunchKernelGGL((sg_wpr_kernel<O, T, 4, false>), dim3(grid), dim3(512), kWprWgLds, s, p, wl)
     if (open) {
         if (p.tls) SG_WPR_LAUNCH(true, true); else SG_WPR_LAUNCH(true, false);
     } else {
         if (p.tls) SG_WPR_LAUNCH(false, true); else SG_WPR_LAUNCH(false, false);
+    }
+#undef SG_WPR_LAUNCH
+    return hipGetLastError();
+}
+
+hipError_t launch_wpr_keying_lists(const KParams& p, bool open, const WprList* wl, hipStream_t s) {
+    if (!p.tls) return hipErrorInvalidValue;  // buckets are TLS records
+    WprKeyJobs jobs = {};
+    uint32_t grid = 0;
+    for (uint32_t b = 0; b < kWprBuckets; ++b) {
+        if (wl[b].count == 0) continue;
+        jobs.b[jobs.njobs] = wl[b];
+        jobs.blk0[jobs.njobs] = grid;
+        grid += (wl[b].count + kWprKeyThreads - 1u) / kWprKeyThreads;
+        ++jobs.njobs;
+    }
+    if (grid == 0) return hipSuccess;
+    if (open)
+        hipLaunchKernelGGL((sg_wpr_keying_kernel<true, true>), dim3(grid), dim3(kWprKeyThreads), 0, s, p, jobs);
+    else
+        hipLaunchKernelGGL((sg_wpr_keying_kernel<false, true>), dim3(grid), dim3(kWprKeyThreads), 0, s, p, jobs);
+    return hipGetLastError();
+}
+
+hipError_t launch_wpr_list(const KParams& p, bool open, uint32_t J, const WprList& wl, hipStream_t s) {
+    if (wl.count == 0) return hipSuccess;
+    if (!p.tls || J < kWprMinJ || J > 4u) return hipErrorInvalidValue;  // buckets are TLS records of 2..4 chunks
+    hipError_t e;
+    int cus = 0;
+    if ((e = device_cus(&cus)) != hipSuccess) return e;
+    const uint32_t grid = wpr_grid(cus, wl.count);
+#define SG_WPR_LAUNCH(O, JJ) hipLaunchKernelGGL((sg_wpr_kernel<O, true, JJ, true>), dim3(grid), dim3(512), kWprWgLds, s, p, wl)
+    switch (J) {
+        case 2: if (open) SG_WPR_LAUNCH(true, 2); else SG_WPR_LAUNCH(false, 2); break;
+        case 3: if (open) SG_WPR_LAUNCH(true, 3); else SG_WPR_LAUNCH(false, 3); break;
+        default: if (open) SG_WPR_LAUNCH(true, 4); else SG_WPR_LAUNCH(false, 4); break;
     }
 #undef SG_WPR_LAUNCH
     return hipGetLastError();

@@ -545,3 +545,115 @@ def test_single_record_limits(gpu, oracle):
     big = bytes(32769)
     assert lib.sg_seal(enc._ptr, nonce, 8, big, len(big), ad, 13, out) == N.SG_E_ARG
     assert lib.sg_open(dec._ptr, nonce, 8, big + bytes(16), len(big) + 16, ad, 13, out) == N.SG_E_ARG
+
+
+def _mixed_wpr_layout(count, rng, aligned=True):
+    """Lengths that fill every wave-per-record bucket (4 KiB < n <= 16 KiB,
+    multiples of 64: J = 2, 3, 4 chunks, their edges) and the size classes
+    around them (n <= 4096, n not a multiple of 64); records packed at 16-byte
+    (or, aligned=False, odd) offsets."""
+    edges = [4096, 4160, 8192, 8256, 12288, 12352, 16320, 16384, 5000, 4097, 16383, 64, 0, 1, 2049]
+    lens = np.where(rng.random(count) < 0.75, 64 * rng.integers(65, 257, size=count),
+                    rng.integers(0, 16385, size=count)).astype(np.uint32)
+    lens[:len(edges)] = edges
+    pad = 16 if aligned else 1
+    step_i = ((lens.astype(np.uint64) + pad - 1) // pad) * pad + (0 if aligned else 3)
+    step_o = ((lens.astype(np.uint64) + 16 + pad - 1) // pad) * pad + (0 if aligned else 5)
+    in_off = np.zeros(count, dtype=np.uint64)
+    out_off = np.zeros(count, dtype=np.uint64)
+    in_off[1:] = np.cumsum(step_i[:-1])
+    out_off[1:] = np.cumsum(step_o[:-1])
+    return lens, in_off, out_off, int(in_off[-1] + step_i[-1]), int(out_off[-1] + step_o[-1])
+
+
+@pytest.mark.parametrize("count", [600, 24000])
+def test_mixed_batch_wave_per_record_buckets(gpu, oracle, count):
+    """Mixed TLS batches whose 4-16 KiB records (multiples of 64 bytes, 16-byte
+    aligned) run on the wave-per-record kernel, right-aligned in its 16 KiB
+    frame (sg_wpr.hip), in three chunk-count buckets; the rest on the size
+    classes.  24000 records put ~6000 in each bucket, more than the two
+    statically assigned groups per workgroup, so the device group counter and
+    the descriptor prefetch run too.  Every byte against the oracle; open with
+    tampering in the first (partial) chunk, the last chunk and the tag of
+    bucket records, and a truncated record."""
+    torch = torch_mod()
+    from suruga_amd import batch as B
+
+    rng = np.random.default_rng(29 + count)
+    lens, in_off, out_off, pt_bytes, ct_bytes = _mixed_wpr_layout(count, rng)
+    buckets = {(int(n) + 4095) // 4096 for n in lens if 4096 < n <= 16384 and n % 64 == 0}
+    assert buckets == {2, 3, 4}
+    keys_h = rng.bytes(256 * 32)
+    kidx = rng.integers(0, 256, size=count).astype(np.uint32)
+    seqs = rng.integers(0, 2**63, size=count, dtype=np.uint64)
+    seqs[:3] = [0, 2**32 - 1, 2**64 - 1]
+    pt_h = rng.bytes(pt_bytes)
+    dev = lambda a: torch.from_numpy(a.view(np.int64) if a.dtype == np.uint64 else a.view(np.int32)).to("cuda")
+    keys = dev_bytes(keys_h).view(256, 32)
+    d_lens, d_olens, d_in, d_out = dev(lens), dev((lens + 16).astype(np.uint32)), dev(in_off), dev(out_off)
+    common = dict(count=count, keys=keys, key_index=dev(kidx), seq=dev(seqs))
+    ct = torch.zeros(ct_bytes, dtype=torch.uint8, device="cuda")
+    B.seal(B.Batch(inp=dev_bytes(pt_h), out=ct, lens=d_lens, max_len=int(lens.max()), in_off=d_in, out_off=d_out,
+                   **common))
+    torch.cuda.synchronize()
+    ct_h = bytearray(host(ct))
+    for i in range(count):
+        k = keys_h[32 * int(kidx[i]):32 * int(kidx[i]) + 32]
+        s, n, o, q = int(seqs[i]), int(lens[i]), int(in_off[i]), int(out_off[i])
+        exp = oracle.seal(k, struct.pack(">Q", s), pt_h[o:o + n], oracle.tls_ad(s, n))
+        assert bytes(ct_h[q:q + n + 16]) == exp, (i, n)
+    # open: tamper bucket records (J = 2, 3, 4) at their first byte, their last
+    # ciphertext byte, their tag; truncate one record
+    bucket_recs = [i for i in range(count) if 4096 < lens[i] <= 16384 and lens[i] % 64 == 0]
+    tamper = {bucket_recs[0]: 0, bucket_recs[1]: int(lens[bucket_recs[1]]) - 1, bucket_recs[2]: int(lens[bucket_recs[2]]) + 7}
+    for i, at in tamper.items():
+        ct_h[int(out_off[i]) + at] ^= 0x40
+    olens = (lens + 16).astype(np.uint32)
+    short = bucket_recs[3]
+    olens[short] = 15
+    back = torch.zeros(pt_bytes, dtype=torch.uint8, device="cuda")
+    st = torch.full((count,), 0xFF, dtype=torch.uint8, device="cuda")
+    d_olens = dev(olens)
+    B.open_(B.Batch(inp=dev_bytes(bytes(ct_h)), out=back, lens=d_olens, max_len=int(olens.max()), in_off=d_out,
+                    out_off=d_in, status=st, **common))
+    torch.cuda.synchronize()
+    exp_st = bytearray(count)
+    for i in tamper:
+        exp_st[i] = 1
+    exp_st[short] = 2
+    assert host(st) == bytes(exp_st)
+    back_h = host(back)
+    for i in range(count):
+        if exp_st[i]:
+            continue
+        o, n = int(in_off[i]), int(lens[i])
+        assert back_h[o:o + n] == pt_h[o:o + n], (i, n)
+    # the reference decrypts a tampered record anyway (chacha20_poly1305.rs:80-82):
+    # the plaintext under the flipped byte differs from the input in that byte only
+    i = bucket_recs[0]
+    o = int(in_off[i])
+    assert back_h[o] == pt_h[o] ^ 0x40 and back_h[o + 1:o + int(lens[i])] == pt_h[o + 1:o + int(lens[i])]
+
+
+def test_mixed_batch_unaligned_records_skip_buckets(gpu, oracle):
+    """The same lengths at odd offsets: no record is 16-byte aligned, so every
+    one runs on the size classes (byte-granular where needed); bit-exact."""
+    torch = torch_mod()
+    from suruga_amd import batch as B
+
+    rng = np.random.default_rng(31)
+    count = 300
+    lens, in_off, out_off, pt_bytes, ct_bytes = _mixed_wpr_layout(count, rng, aligned=False)
+    pt_h = rng.bytes(pt_bytes)
+    dev = lambda a: torch.from_numpy(a.view(np.int64) if a.dtype == np.uint64 else a.view(np.int32)).to("cuda")
+    keys = dev_bytes(KEY).view(1, 32)
+    ct = torch.zeros(ct_bytes, dtype=torch.uint8, device="cuda")
+    d_lens, d_in, d_out = dev(lens), dev(in_off), dev(out_off)
+    B.seal(B.Batch(count=count, keys=keys, inp=dev_bytes(pt_h), out=ct, lens=d_lens, max_len=int(lens.max()),
+                   in_off=d_in, out_off=d_out, seq0=5))
+    torch.cuda.synchronize()
+    ct_h = host(ct)
+    for i in range(count):
+        n, o, q = int(lens[i]), int(in_off[i]), int(out_off[i])
+        exp = oracle.seal(KEY, struct.pack(">Q", 5 + i), pt_h[o:o + n], oracle.tls_ad(5 + i, n))
+        assert ct_h[q:q + n + 16] == exp, (i, n)
