@@ -53,6 +53,25 @@ __device__ __forceinline__ void wave_lds_sync() {
     a += b; d ^= a; d = rotl32(d, 8);       \
     c += d; b ^= c; b = rotl32(b, 7);
 
+// Wave-uniform variants for the scalar unit.  The SALU has no rotate and no
+// byte swap: the opaque asm keeps the shift-or from being matched to
+// v_alignbit / v_perm (which would move the whole uniform chain to the VALU).
+__device__ __forceinline__ uint32_t srotl32(uint32_t x, int n) {
+    uint32_t hi = x << n, lo = x >> (32 - n);
+    asm volatile("" : "+s"(hi));
+    return hi | lo;
+}
+__device__ __forceinline__ uint32_t sbswap32(uint32_t x) {
+    uint32_t a = x << 24, b = (x << 8) & 0x00ff0000u;
+    asm volatile("" : "+s"(a), "+s"(b));
+    return a | b | ((x >> 8) & 0x0000ff00u) | (x >> 24);
+}
+#define SG_QR_S(a, b, c, d)                  \
+    a += b; d ^= a; d = srotl32(d, 16);      \
+    c += d; b ^= c; b = srotl32(b, 12);      \
+    a += b; d ^= a; d = srotl32(d, 8);       \
+    c += d; b ^= c; b = srotl32(b, 7);
+
 constexpr uint32_t kSigma0 = 0x61707865u, kSigma1 = 0x3320646eu, kSigma2 = 0x79622d32u, kSigma3 = 0x6b206574u;
 
 // One keystream block (chacha20.rs:25-51 state, :53-109 round20).  k[8] key

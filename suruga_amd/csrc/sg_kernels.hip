@@ -54,18 +54,7 @@ using namespace dev;
 // (3,7,11,15) and the first add of (0,4,8,12) are therefore the same for
 // every block; when the record is wave-uniform (key and nonce in SGPRs) they
 // are computed once on the scalar unit, which otherwise idles, instead of
-// costing ~37 VALU per block.  The SALU has no rotate: the opaque asm keeps the
-// shift-or from being matched to v_alignbit.
-__device__ __forceinline__ uint32_t srotl32(uint32_t x, int n) {
-    uint32_t hi = x << n, lo = x >> (32 - n);
-    asm volatile("" : "+s"(hi));
-    return hi | lo;
-}
-#define SG_QR_S(a, b, c, d)                  \
-    a += b; d ^= a; d = srotl32(d, 16);      \
-    c += d; b ^= c; b = srotl32(b, 12);      \
-    a += b; d ^= a; d = srotl32(d, 8);       \
-    c += d; b ^= c; b = srotl32(b, 7);
+// costing ~37 VALU per block (srotl32 / SG_QR_S, sg_device.h).
 
 struct ChaChaPre {
     uint32_t x[16];  // state after the counter-free part of round 1 (x12 unused)

@@ -39,9 +39,11 @@
 // built once per record as 48-byte digit lines in LDS; a lane reads its
 // 16-byte T fragment as two windows of two adjacent lines (aligned dwords
 // shifted with v_alignbyte).  |D| <
-// 2^23, so with the accumulator seeded at 2^24 every entry is a positive
-// 25-bit integer.  At the end each lane assembles its 16 entries exactly,
-// X = sum_r D[c_r][q] 2^(8 c_r), reduces it mod 2^130 - 5, multiplies by
+// 2^23; the record's first MFMA starts from a zero accumulator and the
+// assembly adds a seed of 2^24 per entry (v_mad_i64_i32 on the signed
+// entries), so every 64-bit word is positive.  At the end each lane assembles
+// its 16 entries exactly, X = sum_r (D[c_r][q] + 2^24) 2^(8 c_r), reduces it
+// mod 2^130 - 5, multiplies by
 // W = r^(4 (31 - q)) (times 2^32 for the upper half-wave) and a DPP sum adds
 // the 64 terms.  The keying kernel supplies the per-record constant ctot:
 // the AD / length blocks, the pad bits, the i8 bias and the seed.  Every step
@@ -342,6 +344,23 @@ __device__ __forceinline__ void dma_chunk(uint32_t l0, const uint8_t* g0) {
         : "memory");
 }
 
+// a * b + c mod 2^64 (a signed, b a wave-uniform multiplier) in one
+// v_mad_i64_i32; the _1 form: a + c with c uniform.  The compiler does not see
+// these as instructions: the first use of an MFMA result goes through
+// mfma_result_fence() (the XDL-write -> VALU-read wait states), and the asm is
+// volatile so that it stays behind the fence.
+__device__ __forceinline__ void mfma_result_fence() { asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory"); }
+__device__ __forceinline__ uint64_t mad_i64_i32(int32_t a, uint32_t b, uint64_t c) {
+    uint64_t d, cc;
+    asm volatile("v_mad_i64_i32 %0, %1, %2, %3, %4" : "=&v"(d), "=s"(cc) : "v"(a), "s"(b), "v"(c));
+    return d;
+}
+__device__ __forceinline__ uint64_t mad_i64_i32_1(int32_t a, uint64_t c) {
+    uint64_t d, cc;
+    asm volatile("v_mad_i64_i32 %0, %1, %2, 1, %3" : "=&v"(d), "=s"(cc) : "v"(a), "s"(c));
+    return d;
+}
+
 // X = sum_m Y_m 2^(64 m) < 2^242 (eight words) -> F26 with limb 4 < 2^27.
 __device__ __forceinline__ F26 reduce_words8(const uint32_t w[8]) {
     // y = (X mod 2^130) + 5 (X >> 130) < 2^131, then once more
@@ -402,6 +421,7 @@ __device__ __forceinline__ u32x4 zero4() {
 // emit s_load (counted on lgkmcnt), so no compiler-counted vector load ever
 // waits behind the kernel's own LDS-DMA queue.
 typedef const __attribute__((address_space(4))) uint32_t* cu32p;
+typedef const __attribute__((address_space(3))) uint32_t* lu32p;
 __device__ __forceinline__ uint32_t cload(const void* base, uint64_t word) {
     return ((cu32p)(uintptr_t)base)[word];
 }
@@ -460,6 +480,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     // the lane's MAC window base (line 5 (1 - hh), dword of byte 47 - q) and shift
     const uint8_t* mac_base = lines + 240u * (1u - hh) + 4u * ((47u - q) >> 2);
     const uint32_t mac_shift = (47u - q) & 3u;
+    // window bases of steps jj >= 2 (mac_lo) and jj < 2 (mac_hi), 64 bytes before
+    // the P window of the step's largest offset
+    uint32_t mac_lo_a = (uint32_t)(uintptr_t)(mac_base - 64), mac_hi_a = (uint32_t)(uintptr_t)(mac_base + 960 - 64);
+    asm volatile("" : "+v"(mac_lo_a), "+v"(mac_hi_a));
+    const lu32p mac_lo = (lu32p)(uintptr_t)mac_lo_a, mac_hi = (lu32p)(uintptr_t)mac_hi_a;
     const uint32_t cnt = wl.count;
     const uint32_t ngroups = (cnt + kWprWaves - 1u) / kWprWaves;
 
@@ -486,8 +511,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
             if constexpr (TLS) {
                 uint64_t seq = p.seq0 + slot;
                 if (p.seq) seq = (uint64_t)cload(p.seq, 2ull * slot) | ((uint64_t)cload(p.seq, 2ull * slot + 1u) << 32);
-                d.n14 = bswap32((uint32_t)(seq >> 32));
-                d.n15 = bswap32((uint32_t)seq);
+                d.n14 = sbswap32((uint32_t)(seq >> 32));  // (on the SALU: the chain below stays scalar)
+                d.n15 = sbswap32((uint32_t)seq);
             } else {
                 d.n14 = cload(p.nonces, 2ull * slot);
                 d.n15 = cload(p.nonces, 2ull * slot + 1u);
@@ -598,11 +623,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
         // and chunk of the record, so they run once per record on the SALU.
         uint32_t u[16] = {kSigma0, kSigma1, kSigma2, kSigma3, kw[0], kw[1], kw[2], kw[3],
                           kw[4],   kw[5],   kw[6],   kw[7],   0u,    0u,    n14,   n15};
-        SG_QR(u[1], u[5], u[9], u[13]) SG_QR(u[2], u[6], u[10], u[14]) SG_QR(u[3], u[7], u[11], u[15])
+        SG_QR_S(u[1], u[5], u[9], u[13]) SG_QR_S(u[2], u[6], u[10], u[14]) SG_QR_S(u[3], u[7], u[11], u[15])
         // and the steps of the double round whose operands are all uniform
         // (tools/gen_chacha_grp.py, SG_CHACHA_DR1S_*; tests/test_chacha_asm_model.py)
         const uint32_t S0 = u[0] + u[4], T1 = u[1] + u[6], T2 = u[2] + u[7];
-        const uint32_t T13 = rotl32(u[13] ^ T2, 16);
+        const uint32_t T13 = srotl32(u[13] ^ T2, 16);
 
         // ---- the keying table has landed (it was followed only by the previous
         // record's tag / status store; the chunk-0 DMA is older)
@@ -661,9 +686,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
         SG_TICK(t_pl);
         SG_ACC(1, t_tw, t_pl);  // W and the digit lines
 
-        i32x16 acc;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) acc[i] = 1 << 24;
+        // The first MFMA of the record starts from a zero accumulator (srcC = 0,
+        // no per-record register initialisation); the 2^24 seed of every entry
+        // is added at the assembly below.
+        i32x16 acc = {};
 
         // MAC step (jj, i): T fragment = the V window of line iv = 5 k + 4 - i for
         // bytes a' < 16 - sigma, else the P window of line iv - 1 (k = (1 - hh) +
@@ -677,9 +703,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
             uint32_t v[5], p[5];
         };
         auto mac_load = [&](uint32_t jj, uint32_t i, MacRaw& R) {
-            const uint8_t* b = mac_base + 480u * (3u - jj) + 48u * (4u - i);
-            const uint32_t* vb = reinterpret_cast<const uint32_t*>(b);
-            const uint32_t* pb = reinterpret_cast<const uint32_t*>(b - 64);
+            // from one of two opaque bases, so that every offset fits ds_read2_b32
+            // (< 1 KiB) and no address is computed on the VALU
+            const uint32_t off = 480u * ((3u - jj) & 1u) + 48u * (4u - i);
+            const lu32p pb = (jj >= 2u ? mac_lo : mac_hi) + off / 4u;
+            const lu32p vb = pb + 16;
             if constexpr (TLS) {
 #pragma unroll
                 for (int t = 0; t < 4; ++t) R.v[t] = vb[t];
@@ -712,11 +740,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
             }
             return f;
         };
-        auto mac_mfma_f = [&](const u32x4& f, const u32x4& a) {
+        auto mac_mfma_f = [&](const u32x4& f, const u32x4& a, bool first = false) {
+            const i32x16 c0 = {};
             acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(__builtin_bit_cast(i32x4, f),
-                                                         __builtin_bit_cast(i32x4, a ^ 0x80808080u), acc, 0, 0, 0);
+                                                         __builtin_bit_cast(i32x4, a ^ 0x80808080u), first ? c0 : acc,
+                                                         0, 0, 0);
         };
-        auto mac_mfma = [&](const MacRaw& R, const u32x4& a) { mac_mfma_f(mac_frag(R), a); };
+        auto mac_mfma = [&](const MacRaw& R, const u32x4& a, bool first = false) { mac_mfma_f(mac_frag(R), a, first); };
         // The MAC of iteration j - 1 runs inside iteration j's rounds: its T
         // windows are read one double round ahead of each MFMA and the MFMAs are
         // two double rounds apart, so neither an LDS latency nor the MFMA chain
@@ -807,7 +837,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
                 gnn = uniform(*gslot);
             }
             if (j > j0) {
-                mac_mfma(R0, A[0]);
+                mac_mfma(R0, A[0], j == j0 + 1u);
                 mac_load(j - 1u, 1u, R1);
             }
             if (pend) {
@@ -920,13 +950,17 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
 #undef SG_DR
 #undef SG_PIN
 
-        // ---- assemble X = sum_r D[c_r][q] 2^(8 c_r - 32 hh), c_r = (r & 3) + 8 (r >> 2) + 4 hh
+        // ---- assemble X = sum_r (D[c_r][q] + 2^24) 2^(8 c_r - 32 hh), c_r = (r & 3) + 8 (r >> 2) + 4 hh
+        // (|D| < 2^23 signed; the seed 2^24 per entry makes every 64-bit word positive)
         uint32_t xw[8];
+        constexpr uint64_t kSeed = (1ull << 24) + (1ull << 32) + (1ull << 40) + (1ull << 48);
+        mfma_result_fence();
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
-            uint64_t yv = (uint64_t)(uint32_t)acc[4 * m + 1] * 256u + (uint32_t)acc[4 * m];
-            yv += (uint64_t)(uint32_t)acc[4 * m + 2] * 65536u;
-            yv += (uint64_t)(uint32_t)acc[4 * m + 3] * 16777216u;
+            uint64_t yv = mad_i64_i32_1(acc[4 * m], kSeed);  // exact mod 2^64: the sum is positive
+            yv = mad_i64_i32(acc[4 * m + 1], 256u, yv);
+            yv = mad_i64_i32(acc[4 * m + 2], 65536u, yv);
+            yv = mad_i64_i32(acc[4 * m + 3], 16777216u, yv);
             xw[2 * m] = (uint32_t)yv;
             xw[2 * m + 1] = (uint32_t)(yv >> 32);
         }

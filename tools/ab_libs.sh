@@ -10,7 +10,7 @@ for i in $(seq 1 "$R"); do
   for spec in "$@"; do
     name=${spec%%=*}; lib=${spec#*=}
     if [ "$lib" = "-" ]; then lib=suruga_amd/libsuruga_gpu.so; fi
-    SURUGA_GPU_LIB=$lib timeout -k 10 300 python bench.py --no-cpu-baseline --steps 10 ${BENCH_ARGS:-} > "$OUT/${name}_$i.json"
+    SURUGA_GPU_LIB=$lib timeout -k 10 300 python bench.py --no-cpu-baseline --steps 10 ${BENCH_ARGS:-} > "$OUT/${name}_$i.json" || echo "$name rc=$?"
     python -c "import json; d=json.loads(open('$OUT/${name}_$i.json').read().strip().splitlines()[-1]); print('$name', '$i', d['value'], 'seal', d['kernel_ms']['seal'], 'open', d['kernel_ms']['open'], 'correct', d['correct'])"
   done
 done

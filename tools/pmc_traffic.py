@@ -29,7 +29,7 @@ def kind(name: str):
     m = re.search(r"(?:aead(?:_list|_ls)?|wpr)_kernel<(false|true)", name)
     if m:
         return "seal" if m.group(1) == "false" else "open"
-    m = re.search(r"(keying|classify)_kernel<(false|true)", name)
+    m = re.search(r"(wpr_keying|keying|classify)_kernel<(false|true)", name)
     if m:
         return f"{m.group(1)}_{'seal' if m.group(2) == 'false' else 'open'}"
     for k in ("compare", "fill"):
@@ -62,14 +62,19 @@ def main(tag: str, records: int = 1 << 20, record_bytes: int = 16384):
             if key not in seen:
                 seen.add(key)
                 acc[k]["dispatch_ns@" + f.parent.name] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
-                base = k.split("_")[-1] if k.startswith(("keying", "classify")) else None
+                base = k.split("_")[-1] if k.startswith(("keying", "wpr_keying", "classify")) else None
+                # a batch has one keying dispatch of each kind it uses: mixed
+                # batches run sg_keying_kernel (and maybe sg_wpr_keying_kernel),
+                # uniform 16 KiB batches sg_wpr_keying_kernel alone
                 if k.startswith("keying"):
                     nbatch[base]["@" + f.parent.name] += 1
+                elif k.startswith("wpr_keying"):
+                    nbatch[base]["@w" + f.parent.name] += 1
                 elif k in ("compare", "fill"):
                     nbatch[k]["@" + f.parent.name] += 1
 
     def batches(k, counter_file):
-        n = nbatch[k].get("@" + counter_file, 0)
+        n = nbatch[k].get("@" + counter_file, 0) or nbatch[k].get("@w" + counter_file, 0)
         return n if n else 1
 
     summ = {}
@@ -78,8 +83,8 @@ def main(tag: str, records: int = 1 << 20, record_bytes: int = 16384):
         for f in sorted(src.glob("pmc_*/run_counter_collection.csv")):
             cols = {r["Counter_Name"] for r in csv.DictReader(open(f)) if kind(r["Kernel_Name"]) == k}
             nb = batches(k, f.parent.name) if k in ("seal", "open", "compare", "fill") else 1
-            if k.startswith(("keying", "classify")):
-                nb = nbatch[k.split("_")[-1]].get("@" + f.parent.name, 1) or 1
+            if k.startswith(("keying", "wpr_keying", "classify")):
+                nb = batches(k.split("_")[-1], f.parent.name)
             for c in cols:
                 out[c] = d[c] / nb
             if "dispatch_ns@" + f.parent.name in d:
