@@ -289,6 +289,15 @@ int sg_timing_read(double* seal_ms, double* open_ms, double* keying_ms,
  * previous setting; a negative argument only queries. */
 int sg_set_lockstep(int enable);
 
+/* Kernel form for the small records of mixed TLS batches (64 B .. 4 KiB, a
+ * multiple of 64 bytes, 16-byte aligned; C2): 1 = the packed kernel (the
+ * 64-byte blocks of 64 consecutive records laid end to end over the lanes,
+ * keyed in the same kernel), 0 = the size-class kernels.  Both are
+ * bit-exact; A/B and test switch like sg_set_lockstep.  Initial value:
+ * environment SG_PACK ("0"/"1"), else 1.  Returns the previous setting; a
+ * negative argument only queries. */
+int sg_set_packed(int enable);
+
 #ifdef __cplusplus
 }
 #endif

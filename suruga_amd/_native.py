@@ -32,7 +32,7 @@ EXPORTS = [
     "sg_ctx_new", "sg_ctx_free", "sg_seal", "sg_open",
     "sg_workspace_size", "sg_seal_batch", "sg_open_batch",
     "sg_fill_records", "sg_compare_records",
-    "sg_last_error", "sg_build_info", "sg_set_timing", "sg_timing_read", "sg_set_lockstep",
+    "sg_last_error", "sg_build_info", "sg_set_timing", "sg_timing_read", "sg_set_lockstep", "sg_set_packed",
     "sg_wire_bound", "sg_write_records", "sg_read_records", "sg_record_timing",
     "sg_sha256", "sg_hmac_sha256", "sg_prf_new", "sg_prf_get_bytes", "sg_prf_free",
     "sg_derive_keys", "sg_finished_verify_data",
@@ -129,6 +129,8 @@ def _declare(lib: C.CDLL) -> None:
     lib.sg_set_timing.argtypes = [C.c_int]
     lib.sg_set_lockstep.restype = C.c_int
     lib.sg_set_lockstep.argtypes = [C.c_int]
+    lib.sg_set_packed.restype = C.c_int
+    lib.sg_set_packed.argtypes = [C.c_int]
     lib.sg_timing_read.restype = C.c_int
     d = C.POINTER(C.c_double)
     u = C.POINTER(C.c_uint32)

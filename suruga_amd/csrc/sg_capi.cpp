@@ -225,12 +225,15 @@ int launch_batch(const sg_batch* b, bool open, hipStream_t s, void* ws) {
     // go to the wave-per-record buckets; not under capture (they are launched
     // on the populations read back), and the per-record arrays are read as
     // dwords by the bucket kernels
-    if (!wpr && !uniform && p.tls && sg::wpr_enabled() && max_n > 4096u) {
+    // (the packed kernel, sg_pack.hip, likewise takes the 64 B-4 KiB ones)
+    if (!wpr && !uniform && p.tls && ((sg::wpr_enabled() && max_n > 4096u) || (sg::pack_enabled() && max_n >= 64u))) {
         hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
         SG_HIP(hipStreamIsCapturing(s, &cap));
-        p.wpr_mix = cap == hipStreamCaptureStatusNone &&
-                    ((uintptr_t)b->key_index | (uintptr_t)b->seq | (uintptr_t)b->len | (uintptr_t)b->in_off |
-                     (uintptr_t)b->out_off) % 4u == 0u;
+        const bool ok = cap == hipStreamCaptureStatusNone &&
+                        ((uintptr_t)b->key_index | (uintptr_t)b->seq | (uintptr_t)b->len | (uintptr_t)b->in_off |
+                         (uintptr_t)b->out_off) % 4u == 0u;
+        p.wpr_mix = ok && sg::wpr_enabled() && max_n > 4096u;
+        p.pack_mix = ok && sg::pack_enabled();
     }
 
     hipEvent_t e[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -311,10 +314,13 @@ size_t sg_mac_len(void) { return SG_MAC_LEN; }
 int sg_abi_version(void) { return SG_ABI_VERSION; }
 const char* sg_last_error(void) { return g_err.c_str(); }
 const char* sg_build_info(void) {
+    static const std::string pk = std::string("; small records of mixed batches: ") + sg::pack_kernel_config();
     static const std::string on = std::string("gfx950 ") + sg::wpr_kernel_config() + "; other batches: " +
                                   sg::class_kernel_config();
     static const std::string off = std::string("gfx950 ") + sg::class_kernel_config() + " (wave-per-record kernel off)";
-    return sg::wpr_enabled() ? on.c_str() : off.c_str();
+    static const std::string on_pk = on + pk, off_pk = off + pk;
+    const bool w = sg::wpr_enabled(), k = sg::pack_enabled();
+    return w ? (k ? on_pk.c_str() : on.c_str()) : (k ? off_pk.c_str() : off.c_str());
 }
 size_t sg_workspace_size(uint32_t count) {
     // keying records, one list per size class, the class populations and the
@@ -464,6 +470,7 @@ int sg_compare_records(const uint8_t* a, uint64_t sa, const uint8_t* b, uint64_t
 }
 
 int sg_set_lockstep(int enable) { return sg::set_wpr(enable); }
+int sg_set_packed(int enable) { return sg::set_pack(enable); }
 
 int sg_set_timing(int enable) {
     std::lock_guard<std::mutex> lk(g_timing_mu);

@@ -238,6 +238,47 @@ __device__ __forceinline__ F26 geo_sum(const F26 x, const uint32_t m) {
     return g;
 }
 
+// ---- Poly1305 Horner step with the clamped r, radix 2^32 ------------------
+// h = h0 + h1 2^32 + h2 2^64 + h3 2^96 + h4 2^128 (h4 small).  r0..r3 are the
+// clamped key words: r0 < 2^28, r1..r3 < 2^28 and divisible by 4, so
+// r_j 2^128 == (r_j / 4) * 5 (mod p) and s_j = r_j + (r_j >> 2) stays exact.
+struct H32 {
+    uint32_t h0, h1, h2, h3, h4;
+};
+
+// h = (h + m + pad * 2^128) * r  (partially reduced: h4 <= 4)
+__device__ __forceinline__ void horner_step(H32& h, uint32_t m0, uint32_t m1, uint32_t m2, uint32_t m3,
+                                            uint32_t pad, uint32_t r0, uint32_t r1, uint32_t r2,
+                                            uint32_t r3, uint32_t s1, uint32_t s2, uint32_t s3) {
+    // h += m (poly1305.rs:227 c.add(&h))
+    uint32_t c;
+    const uint32_t a0 = addc(h.h0, m0, 0u, &c);
+    const uint32_t a1 = addc(h.h1, m1, c, &c);
+    const uint32_t a2 = addc(h.h2, m2, c, &c);
+    const uint32_t a3 = addc(h.h3, m3, c, &c);
+    const uint32_t a4 = h.h4 + pad + c;
+    // * r (poly1305.rs:227 .mult(&r)): column sums < 2^63, then one carry ripple
+    const uint64_t d0 = (uint64_t)a0 * r0 + (uint64_t)a1 * s3 + (uint64_t)a2 * s2 + (uint64_t)a3 * s1;
+    const uint64_t d1 = (uint64_t)a0 * r1 + (uint64_t)a1 * r0 + (uint64_t)a2 * s3 + (uint64_t)a3 * s2 +
+                        (uint64_t)a4 * s1;
+    const uint64_t d2 = (uint64_t)a0 * r2 + (uint64_t)a1 * r1 + (uint64_t)a2 * r0 + (uint64_t)a3 * s3 +
+                        (uint64_t)a4 * s2;
+    const uint64_t d3 = (uint64_t)a0 * r3 + (uint64_t)a1 * r2 + (uint64_t)a2 * r1 + (uint64_t)a3 * r0 +
+                        (uint64_t)a4 * s3;
+    const uint32_t e1 = addc((uint32_t)d1, (uint32_t)(d0 >> 32), 0u, &c);
+    const uint32_t e2 = addc((uint32_t)d2, (uint32_t)(d1 >> 32), c, &c);
+    const uint32_t e3 = addc((uint32_t)d3, (uint32_t)(d2 >> 32), c, &c);
+    uint32_t e4 = a4 * r0 + (uint32_t)(d3 >> 32) + c;
+    // fold bits >= 2^130: (e4 >> 2) * 2^130 == (e4 >> 2) * 5
+    const uint32_t f = (e4 >> 2) * 5u;
+    e4 &= 3u;
+    h.h0 = addc((uint32_t)d0, f, 0u, &c);
+    h.h1 = addc(e1, 0u, c, &c);
+    h.h2 = addc(e2, 0u, c, &c);
+    h.h3 = addc(e3, 0u, c, &c);
+    h.h4 = e4 + c;
+}
+
 // ---- per-record parameters ---------------------------------------------------
 struct RecKey {
     uint32_t k[8];

@@ -70,6 +70,7 @@ struct KParams {
     uint32_t tls_hdr;        // content_type | major << 8 | minor << 16
     uint32_t lds_rec_bytes;  // LDS bytes per record slot of the launched size class
     uint32_t wpr_mix;        // mixed batch: route eligible records to the wave-per-record buckets
+    uint32_t pack_mix;       // mixed batch: route eligible small records to the packed kernel (sg_pack.hip)
 };
 
 // Size classes of the AEAD kernel: class c (0..7) holds records of
@@ -83,7 +84,10 @@ constexpr uint32_t kNumClasses = 8;
 // J = ceil(n / 4096) = 2..4 (the record's chunk count), lists kNumClasses + J - 2.
 constexpr uint32_t kWprBuckets = 3;
 constexpr uint32_t kWprMinJ = 2;
-constexpr uint32_t kNumLists = kNumClasses + kWprBuckets;
+// ... and TLS records of 64 B <= n <= 4 KiB, n a multiple of 64, 16-byte
+// aligned, to the packed kernel (sg_pack.hip): list kPackList.
+constexpr uint32_t kPackList = kNumClasses + kWprBuckets;
+constexpr uint32_t kNumLists = kPackList + 1u;
 constexpr uint32_t kListGridPerCU = 8;   // workgroups per CU for list-driven launches
 
 __host__ __device__ inline uint32_t size_class(uint32_t n) {
@@ -110,7 +114,7 @@ constexpr uint32_t kWprN = 16384;
 //   [0, 88 count)                   size-class keying records (by record index)
 //   [88 count, 248 count)           wave-per-record keying records (by slot)
 //   [248 count, 260 count)          wave-per-record descriptors (by slot)
-//   [260 count, 271 count)          kNumLists record lists
+//   [260 count, 272 count)          kNumLists record lists
 //   then kNumLists populations, the over-long count, kWprBuckets + 1 group counters
 constexpr uint32_t kWsWprTab = kKeyRecWords;
 constexpr uint32_t kWsWprDesc = kWsWprTab + kWprRecWords;
@@ -168,6 +172,14 @@ __host__ __device__ inline uint32_t wpr_bucket_of(uint32_t n, uint64_t in_addr, 
     if (n <= 4096u || n > kWprN || (n & 63u) || ((in_addr | out_addr) & 15u)) return 0u;
     return (n + 4095u) >> 12;
 }
+// Eligibility of one record of a mixed batch for the packed small-record kernel.
+__host__ __device__ inline bool pack_ok(uint32_t n, uint64_t in_addr, uint64_t out_addr) {
+    return n >= 64u && n <= 4096u && (n & 63u) == 0u && ((in_addr | out_addr) & 15u) == 0u;
+}
+bool pack_enabled();  // sg_set_packed / SG_PACK environment switch
+int set_pack(int enable);
+hipError_t launch_pack(const KParams& p, bool open, const uint32_t* list, uint32_t count, hipStream_t s);
+const char* pack_kernel_config();
 hipError_t launch_fill(uint8_t* buf, uint64_t stride, uint32_t len, uint32_t count, uint64_t seed,
                        uint64_t j0, hipStream_t s);
 hipError_t launch_compare(const uint8_t* a, uint64_t sa, const uint8_t* b, uint64_t sb, uint32_t len,

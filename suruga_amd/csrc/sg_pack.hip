@@ -1,0 +1,397 @@
+// sg_pack.hip -- gfx950 packed ChaCha20-Poly1305 for the small records of a
+// mixed TLS batch (klutzy/suruga src/cipher/chacha20_poly1305.rs:48-94 on
+// records of 64 B .. 4 KiB, a multiple of 64 bytes: the C2 sizes below the
+// wave-per-record buckets of sg_wpr.hip).
+//
+// The size-class kernels (sg_kernels.hip) give every record a power-of-two
+// number of lanes, so a record of 33 blocks occupies a 64-lane wave, and they
+// need a keying pre-pass whose 352-byte record per record goes through HBM.
+// Here a 512-thread workgroup takes a run of 128 consecutive records of the
+// list and lays their 64-byte blocks end to end: chunk c of the run is blocks
+// 64 c .. 64 c + 63, lane t of the chunk computes keystream block j + 1 of the
+// record that owns run block 64 c + t (j its block index in the record,
+// chacha20.rs:111-135), and wave w takes chunks w, w + 8, ..., so no lane
+// idles except in the run's last chunk and the last round.  The eight waves
+// run the rounds in lock-step (grouped ARX asm with an s_barrier per rotate
+// group, sg_chacha_grp.inc, as the wave-per-record kernel): the two waves of
+// a SIMD then issue their full-rate add / xor back to back.
+//
+//   setup (waves 0-1, one lane per record): keystream block 0 -> r, s
+//     (chacha20_poly1305.rs:50-52, poly1305.rs:197-203), the powers
+//     hi[a] = r^(1 + 32 a) and lo[b] = r^(4 b) (a, b < 8), the record's
+//     constant term, its first run block and the start bitmap of the run;
+//   chunks (all waves): XOR the record bytes, store, and add the lane's
+//     Poly1305 term into the record's LDS accumulator;
+//   finish (waves 0-1, one lane per record): tag = (acc + constant) + s,
+//     appended (seal, :55) or compared in constant time (open, :84-93).
+//
+// MAC (poly1305.rs:207-228 over ad || le64(13) || ct || le64(n),
+// chacha20_poly1305.rs:19-42).  With the 13-byte TLS AD the ciphertext starts
+// at stream byte 21 = 16 + 5, and with n = 64 nb the stream has B = 4 nb + 2
+// blocks, the last one 13 bytes long.  Lane j's 64 ciphertext bytes are the
+// last 11 bytes of block 4 j + 1, blocks 4 j + 2 .. 4 j + 4 whole and the
+// first 5 bytes of block 4 j + 5; as values v1..v5 (the lane's bytes at their
+// positions in the blocks) its share of h is
+//   Q_j r^(1 + 4 (nb - 1 - j)),  Q_j = sum_k (v_k + [k < 5] 2^128) r^(5 - k),
+// every full block's pad 2^128 counted by the lane that holds the block's last
+// byte.  Q_j is a four-step Horner with the clamped r in radix 2^32 (as the
+// size-class kernels), the weight W = hi[i >> 3] lo[i & 7] (i = nb - 1 - j)
+// one radix-2^26 product.  What no lane holds -- block 0 (AD bytes 0-12,
+// le64(13) bytes 0-2) with its pad, and the last block's le64(n) and pad --
+// is the constant term
+//   (block0 + 2^128) r^B + (n 2^40 + 2^104) r
+// (block 1 starts with le64(13) bytes 3-7, which are zero).  The terms are
+// fully reduced (limbs < 2^26) before the LDS atomics, so the at most 64 terms
+// of a record sum below 2^32 per limb; every step is exact mod 2^130 - 5 and
+// the tag is the reference's bit for bit.
+#include "sg_internal.h"
+#include "sg_device.h"
+#include "sg_chacha_grp.inc"  // grouped ChaCha20 double round (tools/gen_chacha_grp.py --product)
+
+#include <stdint.h>
+#include <stdlib.h>
+
+namespace sg {
+namespace {
+
+using namespace dev;
+
+constexpr uint32_t kPackRecs = 128;                // records per workgroup run
+constexpr uint32_t kPackWaves = 8;                 // two per SIMD: lock-step pairs
+constexpr uint32_t kPackThreads = 64u * kPackWaves;
+constexpr uint32_t kPackBlocks = kPackRecs * 64u;  // run blocks at most (nb <= 64)
+constexpr uint32_t kPackChunks = kPackBlocks / 64u;
+constexpr uint32_t kSlotWords = 36;                // record slot stride (bank spread)
+constexpr uint32_t kTabWords = 81;                 // hi[8] lo[8] x 5 limbs, + 1 (bank spread)
+// slot layout (u32 words)
+constexpr uint32_t kSKey = 0;     // key[8]
+constexpr uint32_t kSN14 = 8, kSN15 = 9;
+constexpr uint32_t kSR = 12;      // r0..r3 (clamped, radix 2^32)
+constexpr uint32_t kSIn = 16;     // in_off lo, hi
+constexpr uint32_t kSOut = 18;    // out_off lo, hi
+constexpr uint32_t kSS = 20;      // s[4]
+constexpr uint32_t kSCtot = 24;   // constant term (5 limbs)
+constexpr uint32_t kSNb = 29, kSStart = 30, kSRec = 31;
+
+struct PackLds {
+    uint32_t slot[kPackRecs * kSlotWords];
+    uint32_t tab[kPackRecs * kTabWords];
+    uint32_t acc[kPackRecs * 5];
+    uint32_t bits[kPackBlocks / 32];  // run block b starts a record
+    uint32_t base[kPackChunks];       // first-chunk histogram, then records starting before chunk c
+    uint32_t wtot;                    // wave 0's blocks (setup scan)
+    uint32_t nchunks, total;
+};
+static_assert(sizeof(PackLds) <= 65536, "static LDS");
+
+// inclusive prefix sum over the 64 lanes of a wave
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, uint32_t lane) {
+#pragma unroll
+    for (uint32_t d = 1; d < 64u; d <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
+        if (lane >= d) x += y;
+    }
+    return x;
+}
+
+// The record's 64-byte block d[16] (ciphertext words) as the Poly1305 values
+// v1..v5 of the header comment, the MAC stream shifted by 5 bytes:
+// stream word w of the lane is alignbyte(d[w - 1], d[w - 2], 3).
+__device__ __forceinline__ void lane_mac(H32& h, const uint32_t d[16], uint32_t r0, uint32_t r1, uint32_t r2,
+                                         uint32_t r3, uint32_t s1, uint32_t s2, uint32_t s3) {
+    uint32_t e[18];
+    e[0] = 0u;
+    e[1] = d[0] << 8;
+#pragma unroll
+    for (int w = 2; w < 17; ++w) e[w] = __builtin_amdgcn_alignbyte(d[w - 1], d[w - 2], 3);
+    e[17] = d[15] >> 24;
+    h = H32{0u, 0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int k = 0; k < 4; ++k)  // (h + v_k + 2^128) r
+        horner_step(h, e[4 * k], e[4 * k + 1], e[4 * k + 2], e[4 * k + 3], 1u, r0, r1, r2, r3, s1, s2, s3);
+    uint32_t c;  // + v5 (no pad: block 4 j + 5 ends in the next lane or is the last block)
+    h.h0 = addc(h.h0, e[16], 0u, &c);
+    h.h1 = addc(h.h1, e[17], c, &c);
+    h.h2 = addc(h.h2, 0u, c, &c);
+    h.h3 = addc(h.h3, 0u, c, &c);
+    h.h4 += c;
+}
+
+// Phase timing (experiment builds only, -DSG_PACK_PROFILE=1; output
+// unchanged): s_memtime stamps of waves 0 and 7 of the first kProfWgs
+// workgroups, read back by tools/pack_phase.py through sg_pack_profile_read.
+#ifndef SG_PACK_PROFILE
+#define SG_PACK_PROFILE 0
+#endif
+constexpr uint32_t kProfWgs = 8192, kProfStamps = 8;
+#if SG_PACK_PROFILE
+__device__ unsigned long long g_pack_prof[kProfWgs][kProfStamps];
+#define SG_STAMP(w, k)                                                                              \
+    do {                                                                                            \
+        const uint64_t t_ = __builtin_amdgcn_s_memtime();                                           \
+        if (wave == (w) && lane == 0u && blockIdx.x < kProfWgs) g_pack_prof[blockIdx.x][k] = t_;     \
+    } while (0)
+#else
+#define SG_STAMP(w, k)
+#endif
+
+template <bool OPEN>
+__global__ __launch_bounds__(kPackThreads) void sg_pack_kernel(const KParams p, const uint32_t* __restrict__ list,
+                                                               const uint32_t count) {
+    __shared__ PackLds L;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = uniform(tid >> 6);
+    // XCD-aware run order (as the list kernels): workgroup b runs on XCD b % 8
+    const uint32_t ng = gridDim.x, x8 = blockIdx.x & 7u, q8 = ng >> 3, r8 = ng & 7u;
+    const uint32_t run = x8 * q8 + (x8 < r8 ? x8 : r8) + (blockIdx.x >> 3);
+    const uint32_t first = run * kPackRecs;
+    const uint32_t nrec = count - first < kPackRecs ? count - first : kPackRecs;
+
+    SG_STAMP(0u, 0);
+    for (uint32_t i = tid; i < kPackBlocks / 32u; i += kPackThreads) L.bits[i] = 0u;
+    for (uint32_t i = tid; i < kPackRecs * 5u; i += kPackThreads) L.acc[i] = 0u;
+    if (tid < kPackChunks) L.base[tid] = 0u;
+
+    // ---- setup: lane m of waves 0-1 keys record m of the run ---------------------
+    // (a) everything but the record's place in the run: the loads first, as
+    // three levels (list -> per-record arrays -> key words), then block 0, the
+    // powers and the constant term
+    const uint32_t m0 = tid;  // waves 0-1
+    const bool act = m0 < nrec;
+    uint32_t nb = 0u, start = 0u;
+    if (wave < 2u) {
+        const uint32_t rec = act ? list[first + m0] : 0u;
+        uint32_t* sl = L.slot + m0 * kSlotWords;
+        uint32_t* tb = L.tab + m0 * kTabWords;
+        if (act) {
+            const uint32_t len = record_len(p, rec);
+            const uint64_t io = p.in_off ? p.in_off[rec] : p.in_stride * rec;
+            const uint64_t oo = p.out_off ? p.out_off[rec] : p.out_stride * rec;
+            const RecKey rk = record_key(p, rec);
+            const uint32_t n = OPEN ? len - 16u : len;  // listed records: 64 <= n <= 4096, n % 64 == 0
+            nb = n >> 6;
+            uint32_t ks[16];
+            chacha_block(ks, rk.k, 0u, rk.n14, rk.n15);  // block 0 -> poly key (chacha20_poly1305.rs:50,75)
+            // r = clamp(pk[0..16]) (poly1305.rs:197-203), s = pk[16..32] (chacha20_poly1305.rs:32-39)
+            const uint32_t r0 = ks[0] & 0x0fffffffu, r1 = ks[1] & 0x0ffffffcu;
+            const uint32_t r2w = ks[2] & 0x0ffffffcu, r3 = ks[3] & 0x0ffffffcu;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) sl[kSKey + i] = rk.k[i];
+            sl[kSN14] = rk.n14;
+            sl[kSN15] = rk.n15;
+            sl[kSR + 0] = r0; sl[kSR + 1] = r1; sl[kSR + 2] = r2w; sl[kSR + 3] = r3;
+            sl[kSIn] = (uint32_t)io; sl[kSIn + 1] = (uint32_t)(io >> 32);
+            sl[kSOut] = (uint32_t)oo; sl[kSOut + 1] = (uint32_t)(oo >> 32);
+            sl[kSS + 0] = ks[4]; sl[kSS + 1] = ks[5]; sl[kSS + 2] = ks[6]; sl[kSS + 3] = ks[7];
+            sl[kSNb] = nb;
+            sl[kSRec] = rec;
+            // hi[a] = r^(1 + 32 a), lo[b] = R^b (R = r^4)
+            const F26 r = words_to_f26(r0, r1, r2w, r3, 0u);
+            const F26 r2 = fmul(r, r), R = fmul(r2, r2);
+            F26 y = f26_one();
+#pragma unroll
+            for (int b = 0; b < 8; ++b) {
+                store_f26(tb + 40u + 5u * b, y);
+                y = fmul(y, R);
+            }
+            const F26 R8 = y;  // r^32
+            F26 z = r;
+#pragma unroll
+            for (int a = 0; a < 8; ++a) {
+                store_f26(tb + 5u * a, z);
+                if (a < 7) z = fmul(z, R8);
+            }
+            // constant term (header comment): r^B = r^(4 nb + 2) = W(nb - 1) R r
+            const uint32_t il = nb - 1u;
+            const F26 wl = fmul(load_f26(tb + 5u * (il >> 3)), load_f26(tb + 40u + 5u * (il & 7u)));
+            const F26 rB = fmul(fmul(wl, R), r);
+            // block 0: be64(seq) || type || major || minor || be16(n) || le64(13)[0..3] (tls.rs:103-112)
+            const uint32_t w2 = (p.tls_hdr & 0x00ffffffu) | (((n >> 8) & 0xffu) << 24);
+            const uint32_t w3 = (n & 0xffu) | (13u << 8);
+            const F26 blk0 = words_to_f26(rk.n14, rk.n15, w2, w3, 1u);   // + the pad 2^128
+            const F26 sfx = words_to_f26(0u, n << 8, 0u, 256u, 0u);      // n 2^40 + 2^104
+            store_f26(sl + kSCtot, fmul_add(blk0, rB, fmul(sfx, r)));
+        }
+        const uint32_t incl = wave_incl_scan(nb, lane);
+        start = incl - nb;
+        if (wave == 0u && lane == 63u) L.wtot = incl;
+    }
+    SG_STAMP(0u, 1);
+    __syncthreads();
+    // (b) the record's first run block: the start bitmap and first-chunk histogram
+    if (wave < 2u) {
+        if (wave == 1u) start += L.wtot;
+        if (act) {
+            L.slot[m0 * kSlotWords + kSStart] = start;
+            atomicOr(&L.bits[start >> 5], 1u << (start & 31u));
+            atomicAdd(&L.base[start >> 6], 1u);
+        }
+    }
+    __syncthreads();
+    // (c) base[c]: records whose first block lies before chunk c (exclusive scan
+    // of the first-chunk histogram, two chunks per lane)
+    if (wave == 0u) {
+        const uint32_t h0 = L.base[2u * lane], h1 = L.base[2u * lane + 1u];
+        const uint32_t incl = wave_incl_scan(h0 + h1, lane);
+        L.base[2u * lane] = incl - h0 - h1;
+        L.base[2u * lane + 1u] = incl - h1;
+    }
+    if (wave == 1u && lane == 63u) {
+        const uint32_t total = start + nb;  // the run's last record (or an empty lane) ends the run
+        L.total = total;
+        L.nchunks = (total + 63u) >> 6;
+    }
+    __syncthreads();
+
+    // ---- chunk rounds: wave w takes chunk 8 k + w in round k --------------------
+    // Every wave runs every round's ChaCha20 double rounds (grouped by kind,
+    // s_barrier after each rotate group: the two waves of a SIMD issue their
+    // full-rate add / xor back to back, sg_chacha_grp.inc), also in a round with
+    // no chunk for it, so that all waves meet the same barriers.
+    SG_STAMP(0u, 2);
+    SG_STAMP(7u, 6);
+    const uint32_t total = L.total, nchunks = L.nchunks;
+    const uint32_t nrounds = (nchunks + kPackWaves - 1u) / kPackWaves;
+    for (uint32_t k = 0; k < nrounds; ++k) {
+        const uint32_t c = kPackWaves * k + wave;
+        const uint32_t b = 64u * c + lane;
+        const bool valid = c < nchunks && b < total;
+        // the record of run block b: the starts at or before it
+        uint32_t m = 0u;
+        if (c < nchunks) {
+            const uint32_t mlo = L.bits[2u * c], mhi = L.bits[2u * c + 1u];
+            const uint32_t below = __builtin_amdgcn_mbcnt_hi(mhi, __builtin_amdgcn_mbcnt_lo(mlo, 0u));
+            const uint32_t own = ((lane < 32u ? mlo >> lane : mhi >> (lane - 32u)) & 1u);
+            m = L.base[c] + below + own - 1u;
+        }
+        if (!valid) m = 0u;
+        const uint32_t* sl = L.slot + m * kSlotWords;
+        const uint32_t j = b - sl[kSStart];
+        const uint64_t io = (uint64_t)sl[kSIn] | ((uint64_t)sl[kSIn + 1] << 32);
+        const uint64_t oo = (uint64_t)sl[kSOut] | ((uint64_t)sl[kSOut + 1] << 32);
+        u32x4 d0 = {}, d1 = {}, d2 = {}, d3 = {};
+        if (valid) {
+            const uint8_t* src = p.in + io + 64u * j;
+            d0 = ld16(src); d1 = ld16(src + 16); d2 = ld16(src + 32); d3 = ld16(src + 48);
+        }
+        uint32_t kw[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) kw[i] = sl[kSKey + i];
+        const uint32_t ctr = j + 1u, n14 = sl[kSN14], n15 = sl[kSN15];  // data uses blocks 1.. (chacha20_poly1305.rs:52)
+        uint32_t x[16] = {kSigma0, kSigma1, kSigma2, kSigma3, kw[0], kw[1], kw[2], kw[3],
+                          kw[4],   kw[5],   kw[6],   kw[7],   ctr,     0u,    n14,   n15};
+#pragma unroll
+        for (int dr = 0; dr < 10; ++dr) {
+            asm volatile(SG_CHACHA_DR_NB1_BAR1
+                         : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]),
+                           "+v"(x[7]), "+v"(x[8]), "+v"(x[9]), "+v"(x[10]), "+v"(x[11]), "+v"(x[12]), "+v"(x[13]),
+                           "+v"(x[14]), "+v"(x[15]));
+        }
+        if (valid) {
+            // feed-forward (chacha20.rs:104-106) and XOR (chacha20.rs:143-153)
+            const u32x4 o0 = d0 ^ u32x4{x[0] + kSigma0, x[1] + kSigma1, x[2] + kSigma2, x[3] + kSigma3};
+            const u32x4 o1 = d1 ^ u32x4{x[4] + kw[0], x[5] + kw[1], x[6] + kw[2], x[7] + kw[3]};
+            const u32x4 o2 = d2 ^ u32x4{x[8] + kw[4], x[9] + kw[5], x[10] + kw[6], x[11] + kw[7]};
+            const u32x4 o3 = d3 ^ u32x4{x[12] + ctr, x[13], x[14] + n14, x[15] + n15};
+            uint8_t* dst = p.out + oo + 64u * j;
+            st16(dst, o0);
+            st16(dst + 16, o1);
+            st16(dst + 32, o2);
+            st16(dst + 48, o3);
+            // the MAC reads the ciphertext: received (open) or produced (seal)
+            const u32x4 a0 = OPEN ? d0 : o0, a1 = OPEN ? d1 : o1, a2 = OPEN ? d2 : o2, a3 = OPEN ? d3 : o3;
+            const uint32_t cw[16] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3],
+                                     a2[0], a2[1], a2[2], a2[3], a3[0], a3[1], a3[2], a3[3]};
+            const uint32_t r0 = sl[kSR + 0], r1 = sl[kSR + 1], r2 = sl[kSR + 2], r3 = sl[kSR + 3];
+            H32 h;
+            lane_mac(h, cw, r0, r1, r2, r3, r1 + (r1 >> 2), r2 + (r2 >> 2), r3 + (r3 >> 2));
+            const F26 Q = words_to_f26(h.h0, h.h1, h.h2, h.h3, h.h4);
+            const uint32_t i = sl[kSNb] - 1u - j;
+            const uint32_t* tb = L.tab + m * kTabWords;
+            const F26 W = fmul(load_f26(tb + 5u * (i >> 3)), load_f26(tb + 40u + 5u * (i & 7u)));
+            const F26 t = ripple_full(fmul(Q, W));
+            uint32_t* ac = L.acc + 5u * m;
+            atomicAdd(ac + 0, t.v0);
+            atomicAdd(ac + 1, t.v1);
+            atomicAdd(ac + 2, t.v2);
+            atomicAdd(ac + 3, t.v3);
+            atomicAdd(ac + 4, t.v4);
+        }
+    }
+    SG_STAMP(0u, 3);
+    SG_STAMP(7u, 7);
+    __syncthreads();
+    SG_STAMP(0u, 4);
+
+    // ---- finish: one lane per record (waves 0-1) --------------------------------
+    if (act) {
+        const uint32_t* sl = L.slot + m0 * kSlotWords;
+        const uint32_t n = 64u * sl[kSNb], rec = sl[kSRec];
+        const uint32_t* ac = L.acc + 5u * m0;
+        F26 f = carry1(F26{ac[0], ac[1], ac[2], ac[3], ac[4]});
+        f = carry1(f26_add(f, load_f26(sl + kSCtot)));
+        const uint32_t s[4] = {sl[kSS + 0], sl[kSS + 1], sl[kSS + 2], sl[kSS + 3]};
+        uint32_t tw[4];
+        tag_words(f, s, tw);
+        const uint64_t io = (uint64_t)sl[kSIn] | ((uint64_t)sl[kSIn + 1] << 32);
+        const uint64_t oo = (uint64_t)sl[kSOut] | ((uint64_t)sl[kSOut + 1] << 32);
+        if constexpr (!OPEN) {
+            st16(p.out + oo + n, u32x4{tw[0], tw[1], tw[2], tw[3]});  // ct || tag (chacha20_poly1305.rs:55)
+        } else {
+            // constant-time compare: diff |= a ^ b over all 16 bytes (chacha20_poly1305.rs:84-87)
+            const u32x4 rx = ld16(p.in + io + n);
+            const uint32_t diff = (rx[0] ^ tw[0]) | (rx[1] ^ tw[1]) | (rx[2] ^ tw[2]) | (rx[3] ^ tw[3]);
+            p.status[rec] = diff != 0u ? 1u : 0u;
+        }
+    }
+    SG_STAMP(0u, 5);
+}
+
+}  // namespace
+
+hipError_t launch_pack(const KParams& p, bool open, const uint32_t* list, uint32_t count, hipStream_t s) {
+    if (count == 0) return hipSuccess;
+    if (!p.tls) return hipErrorInvalidValue;  // the MAC geometry is the 13-byte TLS AD's
+    const uint32_t grid = (count + kPackRecs - 1u) / kPackRecs;
+    if (open)
+        hipLaunchKernelGGL((sg_pack_kernel<true>), dim3(grid), dim3(kPackThreads), 0, s, p, list, count);
+    else
+        hipLaunchKernelGGL((sg_pack_kernel<false>), dim3(grid), dim3(kPackThreads), 0, s, p, list, count);
+    return hipGetLastError();
+}
+
+#if SG_PACK_PROFILE
+extern "C" int sg_pack_profile_read(unsigned long long* host, size_t n) {
+    const size_t bytes = sizeof(g_pack_prof);
+    if (n * sizeof(unsigned long long) < bytes) return -1;
+    if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_pack_prof), bytes) != hipSuccess) return -2;
+    return (int)(bytes / sizeof(unsigned long long));
+}
+#endif
+
+#ifndef SG_PACK_DEFAULT
+#define SG_PACK_DEFAULT 1
+#endif
+static int g_pack = -1;  // -1: not read from the environment yet
+bool pack_enabled() {
+    if (__atomic_load_n(&g_pack, __ATOMIC_ACQUIRE) < 0) {
+        const char* e = getenv("SG_PACK");
+        int expect = -1;
+        __atomic_compare_exchange_n(&g_pack, &expect, e ? (e[0] == '1' ? 1 : 0) : (SG_PACK_DEFAULT ? 1 : 0), false,
+                                    __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE);
+    }
+    return __atomic_load_n(&g_pack, __ATOMIC_ACQUIRE) == 1;
+}
+int set_pack(int enable) {
+    const int prev = pack_enabled() ? 1 : 0;
+    if (enable >= 0) __atomic_store_n(&g_pack, enable ? 1 : 0, __ATOMIC_RELEASE);
+    return prev;
+}
+
+const char* pack_kernel_config() {
+    return "sg_pack_kernel v2: mixed-batch TLS records of 64 B-4 KiB (multiples of 64 B) packed 64-byte block per lane "
+           "across 128-record runs (512-thread workgroups, chunk rounds, lock-step grouped ChaCha20 rounds), keying in the same kernel "
+           "(block 0, r^(1+32a) and r^(4b) tables in LDS), per-lane Poly1305 share as a 4-step radix-2^32 Horner times "
+           "r^(1+4i), LDS atomic accumulation, constant term for AD / length / pads";
+}
+
+}  // namespace sg

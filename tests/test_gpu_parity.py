@@ -657,3 +657,90 @@ def test_mixed_batch_unaligned_records_skip_buckets(gpu, oracle):
         n, o, q = int(lens[i]), int(in_off[i]), int(out_off[i])
         exp = oracle.seal(KEY, struct.pack(">Q", 5 + i), pt_h[o:o + n], oracle.tls_ad(5 + i, n))
         assert ct_h[q:q + n + 16] == exp, (i, n)
+
+
+@pytest.fixture(params=[1, 0], ids=["packed", "classes"])
+def small_form(request, gpu):
+    from suruga_amd import _native
+
+    lib = _native.load()
+    prev = lib.sg_set_packed(request.param)
+    assert lib.sg_set_packed(-1) == request.param
+    yield request.param
+    lib.sg_set_packed(prev)
+
+
+@pytest.mark.parametrize("count", [777, 9000])
+def test_mixed_batch_packed_small_records(gpu, oracle, small_form, count):
+    """Mixed TLS batches whose 64 B-4 KiB records (multiples of 64 bytes,
+    16-byte aligned) run on the packed kernel (sg_pack.hip: 64-record runs,
+    blocks end to end over the lanes, keyed in the kernel), beside records of
+    other lengths (size classes) and 4-16 KiB ones (wave-per-record buckets);
+    and the same batch on the size classes (small_form 0).  Every block count
+    1..64 occurs, runs of sixty-four 4 KiB records fill a run's 64 chunks, and
+    the count is not a multiple of the run size.  Every byte against the
+    oracle; open with tampering in the first byte, the last ciphertext byte and
+    the tag of packed records, and a truncated record."""
+    torch = torch_mod()
+    from suruga_amd import batch as B
+
+    rng = np.random.default_rng(41 + count)
+    lens = (64 * rng.integers(1, 65, size=count)).astype(np.uint32)
+    lens[100:300] = 4096                       # whole runs of 64 x 64 blocks
+    lens[300:364] = 64 * (np.arange(64) + 1)   # every block count
+    odd = rng.random(count) < 0.1
+    lens[odd] = rng.integers(0, 4200, size=int(odd.sum())).astype(np.uint32)  # size classes
+    big = rng.random(count) < 0.03
+    lens[big] = (64 * rng.integers(65, 257, size=int(big.sum()))).astype(np.uint32)  # buckets
+    step_i = (lens.astype(np.uint64) + 15) // 16 * 16
+    step_o = (lens.astype(np.uint64) + 16 + 15) // 16 * 16
+    in_off = np.zeros(count, dtype=np.uint64)
+    out_off = np.zeros(count, dtype=np.uint64)
+    in_off[1:] = np.cumsum(step_i[:-1])
+    out_off[1:] = np.cumsum(step_o[:-1])
+    pt_bytes, ct_bytes = int(in_off[-1] + step_i[-1]), int(out_off[-1] + step_o[-1])
+    packed = [i for i in range(count) if 64 <= lens[i] <= 4096 and lens[i] % 64 == 0]
+    assert len(packed) > count // 2
+    keys_h = rng.bytes(256 * 32)
+    kidx = rng.integers(0, 256, size=count).astype(np.uint32)
+    seqs = rng.integers(0, 2**63, size=count, dtype=np.uint64)
+    seqs[:3] = [0, 2**32 - 1, 2**64 - 1]
+    pt_h = rng.bytes(pt_bytes)
+    dev = lambda a: torch.from_numpy(a.view(np.int64) if a.dtype == np.uint64 else a.view(np.int32)).to("cuda")
+    keys = dev_bytes(keys_h).view(256, 32)
+    common = dict(count=count, keys=keys, key_index=dev(kidx), seq=dev(seqs))
+    ct = torch.zeros(ct_bytes, dtype=torch.uint8, device="cuda")
+    B.seal(B.Batch(inp=dev_bytes(pt_h), out=ct, lens=dev(lens), max_len=int(lens.max()), in_off=dev(in_off),
+                   out_off=dev(out_off), **common))
+    torch.cuda.synchronize()
+    ct_h = bytearray(host(ct))
+    for i in range(count):
+        k = keys_h[32 * int(kidx[i]):32 * int(kidx[i]) + 32]
+        s, n, o, q = int(seqs[i]), int(lens[i]), int(in_off[i]), int(out_off[i])
+        exp = oracle.seal(k, struct.pack(">Q", s), pt_h[o:o + n], oracle.tls_ad(s, n))
+        assert bytes(ct_h[q:q + n + 16]) == exp, (i, n)
+    tamper = {packed[0]: 0, packed[1]: int(lens[packed[1]]) - 1, packed[2]: int(lens[packed[2]]) + 9}
+    for i, at in tamper.items():
+        ct_h[int(out_off[i]) + at] ^= 0x08
+    olens = (lens + 16).astype(np.uint32)
+    short = packed[3]
+    olens[short] = 15
+    back = torch.zeros(pt_bytes, dtype=torch.uint8, device="cuda")
+    st = torch.full((count,), 0xFF, dtype=torch.uint8, device="cuda")
+    B.open_(B.Batch(inp=dev_bytes(bytes(ct_h)), out=back, lens=dev(olens), max_len=int(olens.max()),
+                    in_off=dev(out_off), out_off=dev(in_off), status=st, **common))
+    torch.cuda.synchronize()
+    exp_st = bytearray(count)
+    for i in tamper:
+        exp_st[i] = 1
+    exp_st[short] = 2
+    assert host(st) == bytes(exp_st)
+    back_h = host(back)
+    for i in range(count):
+        if exp_st[i]:
+            continue
+        o, n = int(in_off[i]), int(lens[i])
+        assert back_h[o:o + n] == pt_h[o:o + n], (i, n)
+    i = packed[0]  # decrypted anyway (chacha20_poly1305.rs:80-82)
+    o = int(in_off[i])
+    assert back_h[o] == pt_h[o] ^ 0x08 and back_h[o + 1:o + int(lens[i])] == pt_h[o + 1:o + int(lens[i])]
