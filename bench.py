@@ -377,13 +377,25 @@ def main():
     dom_ms = tm[f"{dom}_ms"]
     achieved = alg_bytes / (dom_ms * 1e-3) / 1e9
     traffic, valu, traffic_src = None, None, None
-    tp = Path(args.traffic or ROOT / "profiles" / ("traffic_r02.json" if args.workload == "c1" else
-                                                   "traffic_r02_c2.json"))
-    if tp.exists():
+    # the PMC traffic summary of this exact kernel build and workload (the newest
+    # profiles/traffic_*.json whose build string and record shape match)
+    build = lib.sg_build_info().decode()
+    cands = [Path(args.traffic)] if args.traffic else sorted(
+        (ROOT / "profiles").glob("traffic_*.json"), key=lambda q: q.stat().st_mtime, reverse=True)
+    tp = None
+    for q in cands:
+        try:
+            tq = json.loads(q.read_text())
+        except (ValueError, OSError):
+            continue
+        if tq.get("records") == count and tq.get("record_bytes") == cfg["record_bytes"] and \
+                tq.get("kernels") == build and tq.get(f"{dom}_bytes_per_launch"):
+            tp = q
+            break
+    if tp is not None:
         try:
             tj = json.loads(tp.read_text())
-            if tj.get("records") == count and tj.get("record_bytes") == cfg["record_bytes"] and \
-                    tj.get("kernels", lib.sg_build_info().decode()) == lib.sg_build_info().decode():
+            if True:
                 traffic = tj.get(f"{dom}_bytes_per_launch")
                 traffic_src = (f"profiles/{tp.name}: rocprofv3 PMC FETCH_SIZE x 2 + WRITE_SIZE of this kernel build "
                                "in a separate profiling run (not this run)") if traffic else None
@@ -404,7 +416,8 @@ def main():
     if args.workload == "c1":
         dom_kernel = f"sg_wpr_kernel<{dom.upper()}>" if wpr_on else f"sg_aead_kernel<{dom.upper()}, 256>"
     else:
-        dom_kernel = f"sg_classify_kernel + sg_aead_list_kernel<{dom.upper()}, L=2..256> (one batch)"
+        dom_kernel = (f"sg_classify_kernel + sg_wpr_kernel<{dom.upper()}, J=2..4> + sg_pack_kernel<{dom.upper()}> "
+                      "+ size classes (one batch)")
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline and args.workload == "c1":

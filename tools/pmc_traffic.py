@@ -26,7 +26,7 @@ ROOT = Path(__file__).resolve().parent.parent
 
 
 def kind(name: str):
-    m = re.search(r"(?:aead(?:_list|_ls)?|wpr)_kernel<(false|true)", name)
+    m = re.search(r"(?:aead(?:_list|_ls)?|wpr|pack)_kernel<(false|true)", name)
     if m:
         return "seal" if m.group(1) == "false" else "open"
     m = re.search(r"(wpr_keying|keying|classify)_kernel<(false|true)", name)
