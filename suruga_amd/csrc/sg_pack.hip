@@ -123,7 +123,7 @@ __device__ __forceinline__ void lane_mac(H32& h, const uint32_t d[16], uint32_t 
 #ifndef SG_PACK_PROFILE
 #define SG_PACK_PROFILE 0
 #endif
-constexpr uint32_t kProfWgs = 8192, kProfStamps = 8;
+constexpr uint32_t kProfWgs = 8192, kProfStamps = 12;
 #if SG_PACK_PROFILE
 __device__ unsigned long long g_pack_prof[kProfWgs][kProfStamps];
 #define SG_STAMP(w, k)                                                                              \
@@ -169,11 +169,16 @@ __global__ __launch_bounds__(kPackThreads) void sg_pack_kernel(const KParams p, 
             const RecKey rk = record_key(p, rec);
             const uint32_t n = OPEN ? len - 16u : len;  // listed records: 64 <= n <= 4096, n % 64 == 0
             nb = n >> 6;
+#if SG_PACK_PROFILE
+            if (rk.k[0] == 0x12345678u && rk.seq == 1u) g_pack_prof[0][11] = io + oo;  // wait for the loads
+#endif
+            SG_STAMP(0u, 8);
             uint32_t ks[16];
             chacha_block(ks, rk.k, 0u, rk.n14, rk.n15);  // block 0 -> poly key (chacha20_poly1305.rs:50,75)
             // r = clamp(pk[0..16]) (poly1305.rs:197-203), s = pk[16..32] (chacha20_poly1305.rs:32-39)
             const uint32_t r0 = ks[0] & 0x0fffffffu, r1 = ks[1] & 0x0ffffffcu;
             const uint32_t r2w = ks[2] & 0x0ffffffcu, r3 = ks[3] & 0x0ffffffcu;
+            SG_STAMP(0u, 9);
 #pragma unroll
             for (int i = 0; i < 8; ++i) sl[kSKey + i] = rk.k[i];
             sl[kSN14] = rk.n14;
@@ -184,22 +189,24 @@ __global__ __launch_bounds__(kPackThreads) void sg_pack_kernel(const KParams p, 
             sl[kSS + 0] = ks[4]; sl[kSS + 1] = ks[5]; sl[kSS + 2] = ks[6]; sl[kSS + 3] = ks[7];
             sl[kSNb] = nb;
             sl[kSRec] = rec;
-            // hi[a] = r^(1 + 32 a), lo[b] = R^b (R = r^4)
+            // hi[a] = r^(1 + 32 a), lo[b] = R^b (R = r^4), as a shallow product tree
+            // (critical path 9 products instead of a 17-long chain: the setup
+            // waves are latency-bound)
             const F26 r = words_to_f26(r0, r1, r2w, r3, 0u);
             const F26 r2 = fmul(r, r), R = fmul(r2, r2);
-            F26 y = f26_one();
+            const F26 R2 = fmul(R, R), R3 = fmul(R2, R), R4 = fmul(R2, R2);
+            const F26 R5 = fmul(R4, R), R6 = fmul(R3, R3), R7 = fmul(R4, R3);
+            const F26 R8 = fmul(R4, R4);  // r^32
+            const F26 R16 = fmul(R8, R8), R24 = fmul(R16, R8), R32 = fmul(R16, R16);
+            const F26 R40 = fmul(R32, R8), R48 = fmul(R32, R16), R56 = fmul(R32, R24);
+            const F26 lo[8] = {f26_one(), R, R2, R3, R4, R5, R6, R7};
+            const F26 hs[7] = {R8, R16, R24, R32, R40, R48, R56};
+            store_f26(tb, r);
 #pragma unroll
-            for (int b = 0; b < 8; ++b) {
-                store_f26(tb + 40u + 5u * b, y);
-                y = fmul(y, R);
-            }
-            const F26 R8 = y;  // r^32
-            F26 z = r;
+            for (int a = 1; a < 8; ++a) store_f26(tb + 5u * a, fmul(hs[a - 1], r));
 #pragma unroll
-            for (int a = 0; a < 8; ++a) {
-                store_f26(tb + 5u * a, z);
-                if (a < 7) z = fmul(z, R8);
-            }
+            for (int b = 0; b < 8; ++b) store_f26(tb + 40u + 5u * b, lo[b]);
+            SG_STAMP(0u, 10);
             // constant term (header comment): r^B = r^(4 nb + 2) = W(nb - 1) R r
             const uint32_t il = nb - 1u;
             const F26 wl = fmul(load_f26(tb + 5u * (il >> 3)), load_f26(tb + 40u + 5u * (il & 7u)));

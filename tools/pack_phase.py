@@ -42,13 +42,17 @@ def main():
     for _ in range(3):
         B.seal(b)
     torch.cuda.synchronize()
-    buf = (C.c_ulonglong * (8192 * 8))()
+    buf = (C.c_ulonglong * (8192 * 12))()
     n = lib.sg_pack_profile_read(buf, len(buf))
     assert n > 0, n
-    a = np.frombuffer(buf, dtype=np.uint64).reshape(8192, 8).astype(np.int64)
+    a = np.frombuffer(buf, dtype=np.uint64).reshape(8192, 12).astype(np.int64)
     a = a[a[:, 0] != 0]
     d = lambda i, j: float(np.mean(a[:, j] - a[:, i]))
     print(f"workgroups {len(a)}  (s_memtime ticks)")
+    print(f"  setup: zero + loads                  {d(0, 8):9.0f}")
+    print(f"  setup: block 0                       {d(8, 9):9.0f}")
+    print(f"  setup: slot + tables                 {d(9, 10):9.0f}")
+    print(f"  setup: constant term + scan          {d(10, 1):9.0f}")
     print(f"  setup (wave 0: zero, scan, keying)   {d(0, 1):9.0f}")
     print(f"  setup syncs + base scan              {d(1, 2):9.0f}")
     print(f"  rounds wave 0                        {d(2, 3):9.0f}")
