@@ -61,17 +61,22 @@ constexpr uint32_t kPackWaves = 8;                 // two per SIMD: lock-step pa
 constexpr uint32_t kPackThreads = 64u * kPackWaves;
 constexpr uint32_t kPackBlocks = kPackRecs * 64u;  // run blocks at most (nb <= 64)
 constexpr uint32_t kPackChunks = kPackBlocks / 64u;
-constexpr uint32_t kSlotWords = 36;                // record slot stride (bank spread)
-constexpr uint32_t kTabWords = 81;                 // hi[8] lo[8] x 5 limbs, + 1 (bank spread)
+constexpr uint32_t kSlotWords = 30;                // record slot stride (ds_read_b64, bank spread)
+// weight tables hi[8] lo[8] (entry e: hi[e], lo[e - 8]) as 128-bit words, the
+// top two bits of entry e at bit 2 e of word 64 (odd stride: bank spread), so
+// that three workgroups fit a CU's LDS
+constexpr uint32_t kTabWords = 65;
+constexpr uint32_t kTabTop = 64;
 // slot layout (u32 words)
 constexpr uint32_t kSKey = 0;     // key[8]
 constexpr uint32_t kSN14 = 8, kSN15 = 9;
-constexpr uint32_t kSR = 12;      // r0..r3 (clamped, radix 2^32)
-constexpr uint32_t kSIn = 16;     // in_off lo, hi
-constexpr uint32_t kSOut = 18;    // out_off lo, hi
-constexpr uint32_t kSS = 20;      // s[4]
-constexpr uint32_t kSCtot = 24;   // constant term (5 limbs)
-constexpr uint32_t kSNb = 29, kSStart = 30, kSRec = 31;
+constexpr uint32_t kSR = 10;      // r0..r3 (clamped, radix 2^32)
+constexpr uint32_t kSIn = 14;     // in_off lo, hi
+constexpr uint32_t kSOut = 16;    // out_off lo, hi
+constexpr uint32_t kSS = 18;      // s[4]
+constexpr uint32_t kSCtot = 22;   // constant term (5 limbs)
+constexpr uint32_t kSNb = 27, kSStart = 28, kSRec = 29;
+static_assert(kSRec < kSlotWords, "slot layout");
 
 struct PackLds {
     uint32_t slot[kPackRecs * kSlotWords];
@@ -83,6 +88,25 @@ struct PackLds {
     uint32_t nchunks, total;
 };
 static_assert(sizeof(PackLds) <= 65536, "static LDS");
+static_assert(3 * sizeof(PackLds) <= 160 * 1024, "three workgroups per CU");
+
+// table entry e <- x (fully reduced first; top bits collected by the caller)
+__device__ __forceinline__ uint32_t tab_put(uint32_t* tb, uint32_t e, F26 x) {
+    x = ripple_full(x);  // limbs < 2^26: x < 2^130
+    tb[4u * e + 0] = x.v0 | (x.v1 << 26);
+    tb[4u * e + 1] = (x.v1 >> 6) | (x.v2 << 20);
+    tb[4u * e + 2] = (x.v2 >> 12) | (x.v3 << 14);
+    tb[4u * e + 3] = (x.v3 >> 18) | (x.v4 << 8);
+    return (x.v4 >> 24) << (2u * e);
+}
+__device__ __forceinline__ F26 tab_get(const uint32_t* tb, uint32_t e, uint32_t top) {
+    return words_to_f26(tb[4u * e], tb[4u * e + 1], tb[4u * e + 2], tb[4u * e + 3], (top >> (2u * e)) & 3u);
+}
+// W(i) = r^(1 + 4 i) = hi[i >> 3] lo[i & 7]
+__device__ __forceinline__ F26 tab_weight(const uint32_t* tb, uint32_t i) {
+    const uint32_t top = tb[kTabTop];
+    return fmul(tab_get(tb, i >> 3, top), tab_get(tb, 8u + (i & 7u), top));
+}
 
 // inclusive prefix sum over the 64 lanes of a wave
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, uint32_t lane) {
@@ -189,27 +213,28 @@ __global__ __launch_bounds__(kPackThreads) void sg_pack_kernel(const KParams p, 
             sl[kSS + 0] = ks[4]; sl[kSS + 1] = ks[5]; sl[kSS + 2] = ks[6]; sl[kSS + 3] = ks[7];
             sl[kSNb] = nb;
             sl[kSRec] = rec;
-            // hi[a] = r^(1 + 32 a), lo[b] = R^b (R = r^4), as a shallow product tree
-            // (critical path 9 products instead of a 17-long chain: the setup
-            // waves are latency-bound)
+            // hi[a] = r^(1 + 32 a), lo[b] = R^b (R = r^4), two product chains
             const F26 r = words_to_f26(r0, r1, r2w, r3, 0u);
             const F26 r2 = fmul(r, r), R = fmul(r2, r2);
-            const F26 R2 = fmul(R, R), R3 = fmul(R2, R), R4 = fmul(R2, R2);
-            const F26 R5 = fmul(R4, R), R6 = fmul(R3, R3), R7 = fmul(R4, R3);
-            const F26 R8 = fmul(R4, R4);  // r^32
-            const F26 R16 = fmul(R8, R8), R24 = fmul(R16, R8), R32 = fmul(R16, R16);
-            const F26 R40 = fmul(R32, R8), R48 = fmul(R32, R16), R56 = fmul(R32, R24);
-            const F26 lo[8] = {f26_one(), R, R2, R3, R4, R5, R6, R7};
-            const F26 hs[7] = {R8, R16, R24, R32, R40, R48, R56};
-            store_f26(tb, r);
+            F26 y = f26_one();
+            uint32_t top = 0u;
 #pragma unroll
-            for (int a = 1; a < 8; ++a) store_f26(tb + 5u * a, fmul(hs[a - 1], r));
+            for (int b = 0; b < 8; ++b) {
+                top |= tab_put(tb, 8u + b, y);
+                y = fmul(y, R);
+            }
+            const F26 R8 = y;  // r^32
+            F26 z = r;
 #pragma unroll
-            for (int b = 0; b < 8; ++b) store_f26(tb + 40u + 5u * b, lo[b]);
+            for (int a = 0; a < 8; ++a) {
+                top |= tab_put(tb, a, z);
+                if (a < 7) z = fmul(z, R8);
+            }
+            tb[kTabTop] = top;
             SG_STAMP(0u, 10);
             // constant term (header comment): r^B = r^(4 nb + 2) = W(nb - 1) R r
             const uint32_t il = nb - 1u;
-            const F26 wl = fmul(load_f26(tb + 5u * (il >> 3)), load_f26(tb + 40u + 5u * (il & 7u)));
+            const F26 wl = tab_weight(tb, il);
             const F26 rB = fmul(fmul(wl, R), r);
             // block 0: be64(seq) || type || major || minor || be16(n) || le64(13)[0..3] (tls.rs:103-112)
             const uint32_t w2 = (p.tls_hdr & 0x00ffffffu) | (((n >> 8) & 0xffu) << 24);
@@ -314,7 +339,7 @@ __global__ __launch_bounds__(kPackThreads) void sg_pack_kernel(const KParams p, 
             const F26 Q = words_to_f26(h.h0, h.h1, h.h2, h.h3, h.h4);
             const uint32_t i = sl[kSNb] - 1u - j;
             const uint32_t* tb = L.tab + m * kTabWords;
-            const F26 W = fmul(load_f26(tb + 5u * (i >> 3)), load_f26(tb + 40u + 5u * (i & 7u)));
+            const F26 W = tab_weight(tb, i);
             const F26 t = ripple_full(fmul(Q, W));
             uint32_t* ac = L.acc + 5u * m;
             atomicAdd(ac + 0, t.v0);
