@@ -684,6 +684,8 @@ def test_mixed_batch_packed_small_records(gpu, oracle, small_form, count):
     torch = torch_mod()
     from suruga_amd import batch as B
 
+    # the smaller batch with another record header (AD bytes 8-10, tls.rs:105-112)
+    ctype, minor = (22, 1) if count < 1000 else (23, 3)
     rng = np.random.default_rng(41 + count)
     lens = (64 * rng.integers(1, 65, size=count)).astype(np.uint32)
     lens[100:300] = 4096                       # whole runs of 64 x 64 blocks
@@ -708,7 +710,7 @@ def test_mixed_batch_packed_small_records(gpu, oracle, small_form, count):
     pt_h = rng.bytes(pt_bytes)
     dev = lambda a: torch.from_numpy(a.view(np.int64) if a.dtype == np.uint64 else a.view(np.int32)).to("cuda")
     keys = dev_bytes(keys_h).view(256, 32)
-    common = dict(count=count, keys=keys, key_index=dev(kidx), seq=dev(seqs))
+    common = dict(count=count, keys=keys, key_index=dev(kidx), seq=dev(seqs), content_type=ctype, version=(3, minor))
     ct = torch.zeros(ct_bytes, dtype=torch.uint8, device="cuda")
     B.seal(B.Batch(inp=dev_bytes(pt_h), out=ct, lens=dev(lens), max_len=int(lens.max()), in_off=dev(in_off),
                    out_off=dev(out_off), **common))
@@ -717,7 +719,7 @@ def test_mixed_batch_packed_small_records(gpu, oracle, small_form, count):
     for i in range(count):
         k = keys_h[32 * int(kidx[i]):32 * int(kidx[i]) + 32]
         s, n, o, q = int(seqs[i]), int(lens[i]), int(in_off[i]), int(out_off[i])
-        exp = oracle.seal(k, struct.pack(">Q", s), pt_h[o:o + n], oracle.tls_ad(s, n))
+        exp = oracle.seal(k, struct.pack(">Q", s), pt_h[o:o + n], oracle.tls_ad(s, n, ctype, 3, minor))
         assert bytes(ct_h[q:q + n + 16]) == exp, (i, n)
     tamper = {packed[0]: 0, packed[1]: int(lens[packed[1]]) - 1, packed[2]: int(lens[packed[2]]) + 9}
     for i, at in tamper.items():
