@@ -47,7 +47,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=2.0, help="min wall time of the CPU baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-bitexact", action="store_true",
-                    help="skip the oracle tag fold / sample compare of the last step (C1)")
+                    help="skip the oracle tag fold / sample compare of the last step (C1 and C2)")
     ap.add_argument("--sg-records", type=int, default=16384,
                     help="records per rank moved by the separately timed RCCL scatter/gather (N > 1; 0 = off)")
     ap.add_argument("--strong", action="store_true",
@@ -171,6 +171,42 @@ def bitexact_check(ct, n, count, seq0):
         sample_ok = sample_ok and rows[i].cpu().numpy().tobytes() == exp
     return {"bitexact_fold": fold == ref_fold, "fold_records": count, "bitexact_sample": sample_ok,
             "sample_records": len(idx), "oracle_fold_s": round(fold_s, 2)}
+
+
+def bitexact_check_c2(lay, pt, ct, seq_off):
+    """C2 counterpart of bitexact_check: the XOR-fold of all of the batch's tags
+    (gathered from ct at out_off + len) against the oracle's multithreaded fold
+    of the same records (the device plaintext copied to the host, each record
+    sealed with its connection key and sequence number), plus a byte-for-byte
+    compare of a strided sample of whole records.  Checker only."""
+    import struct
+
+    import numpy as np
+    import torch
+
+    sys.path.insert(0, str(ROOT / "tests"))
+    from oracle_ffi import oracle as get_oracle  # checker only
+
+    o = get_oracle()
+    count = lay.count
+    seqs = lay.seq + np.uint64(seq_off)
+    tag_at = torch.from_numpy((lay.out_off + lay.lens.astype(np.uint64)).view(np.int64)).to(ct.device)
+    idx = (tag_at.view(-1, 1) + torch.arange(16, device=ct.device).view(1, 16)).view(-1)
+    tags = ct[idx].view(count, 16).cpu().numpy()
+    fold = np.bitwise_xor.reduce(tags, axis=0).tobytes()
+    pt_h = pt.cpu().numpy()
+    t0 = time.perf_counter()
+    ref_fold = o.tag_fold_mixed(lay.keys, lay.key_index, seqs, lay.lens, lay.in_off, pt_h, host_threads())
+    fold_s = time.perf_counter() - t0
+    sample = sorted(set([0, 1, count // 2, count - 1] + list(range(0, count, 4099))))
+    ok = True
+    for i in sample:
+        k = lay.keys[32 * int(lay.key_index[i]):32 * int(lay.key_index[i]) + 32]
+        s, n, a, q = int(seqs[i]), int(lay.lens[i]), int(lay.in_off[i]), int(lay.out_off[i])
+        exp = o.seal(k, struct.pack(">Q", s), pt_h[a:a + n].tobytes(), o.tls_ad(s, n))
+        ok = ok and ct[q:q + n + 16].cpu().numpy().tobytes() == exp
+    return {"bitexact_fold": fold == ref_fold, "fold_records": count, "bitexact_sample": ok,
+            "sample_records": len(sample), "oracle_fold_s": round(fold_s, 2)}
 
 
 def measure_scatter_gather(args, dist, backend, rank, world, dev, n, count, seq0, seal_b, lib, keys, ws, stream):
@@ -343,9 +379,10 @@ def main():
     bad_status = int((status != 0).sum().item())
     roundtrip_ok = int(mism.item()) == 0 and bad_status == 0
     exact = None
-    if args.workload == "c1" and not args.no_bitexact:
+    if not args.no_bitexact:
         torch.cuda.synchronize()
-        exact = bitexact_check(ct, n, count, seq0)
+        exact = bitexact_check(ct, n, count, seq0) if args.workload == "c1" else \
+            bitexact_check_c2(lay, pt, ct, seq0 // 256)
         roundtrip_ok = roundtrip_ok and exact["bitexact_fold"] and exact["bitexact_sample"]
 
     # per-kernel device time with HIP events on the launch stream

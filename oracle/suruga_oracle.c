@@ -444,3 +444,58 @@ void so_tag_fold_tls(const uint8_t key[32], uint64_t seq0, uint64_t seed, uint64
     free(jobs);
     free(tids);
 }
+
+/* XOR-fold of the tags of a mixed TLS batch (C2 shape): record i is
+ * pt[in_off[i] .. + lens[i]) sealed with key keys[key_index[i]] and sequence
+ * number seq[i] (tls.rs:103-112, chacha20_poly1305.rs:48-59).  The checker of
+ * bench.py's full-size C2 run.  Test infrastructure only. */
+typedef struct {
+    const uint8_t* keys;
+    const uint32_t* key_index;
+    const uint64_t* seq;
+    const uint32_t* lens;
+    const uint64_t* in_off;
+    const uint8_t* pt;
+    size_t begin, end;
+    uint8_t fold[16];
+} so_mfold_job;
+
+static void* so_mfold_worker(void* arg) {
+    so_mfold_job* j = (so_mfold_job*)arg;
+    uint8_t* ct = (uint8_t*)malloc(65536 + 16);
+    uint8_t nonce[8], ad[13];
+    memset(j->fold, 0, 16);
+    for (size_t i = j->begin; i < j->end; ++i) {
+        const size_t n = j->lens[i];
+        so_u64_be(j->seq[i], nonce);
+        so_tls_ad(j->seq[i], 23, 3, 3, (uint16_t)n, ad);
+        so_seal(j->keys + 32u * j->key_index[i], nonce, j->pt + j->in_off[i], n, ad, 13, ct);
+        for (int b = 0; b < 16; ++b) j->fold[b] ^= ct[n + b];
+    }
+    free(ct);
+    return NULL;
+}
+
+void so_tag_fold_mixed(const uint8_t* keys, const uint32_t* key_index, const uint64_t* seq, const uint32_t* lens,
+                       const uint64_t* in_off, const uint8_t* pt, size_t count, int threads, uint8_t out[16]) {
+    if (threads < 1) threads = 1;
+    if (count > 0 && (size_t)threads > count) threads = (int)count;
+    so_mfold_job* jobs = (so_mfold_job*)calloc((size_t)threads, sizeof(so_mfold_job));
+    pthread_t* tids = (pthread_t*)calloc((size_t)threads, sizeof(pthread_t));
+    size_t per = (count + (size_t)threads - 1) / (size_t)threads;
+    for (int t = 0; t < threads; ++t) {
+        so_mfold_job* j = &jobs[t];
+        j->keys = keys; j->key_index = key_index; j->seq = seq; j->lens = lens; j->in_off = in_off; j->pt = pt;
+        j->begin = (size_t)t * per < count ? (size_t)t * per : count;
+        j->end = j->begin + per < count ? j->begin + per : count;
+        if (threads == 1) so_mfold_worker(j);
+        else pthread_create(&tids[t], NULL, so_mfold_worker, j);
+    }
+    memset(out, 0, 16);
+    for (int t = 0; t < threads; ++t) {
+        if (threads > 1) pthread_join(tids[t], NULL);
+        for (int b = 0; b < 16; ++b) out[b] ^= jobs[t].fold[b];
+    }
+    free(jobs);
+    free(tids);
+}

@@ -93,12 +93,17 @@ void   so_seal_batch_tls(const uint8_t key[32], uint64_t seq0, const uint8_t* pt
 size_t so_open_batch_tls(const uint8_t key[32], uint64_t seq0, const uint8_t* ct,
                          size_t n, size_t count, uint8_t* pt, uint8_t* status, int threads);
 
-#ifdef __cplusplus
-}
-#endif
 /* XOR-fold of the tags of count TLS records (seq = seq0 + i, plaintext =
  * fill-rule record j0 + i) without materialising them. */
 void so_tag_fold_tls(const uint8_t key[32], uint64_t seq0, uint64_t seed, uint64_t j0, size_t n, size_t count,
                      int threads, uint8_t out[16]);
+/* XOR-fold of the tags of a mixed batch: record i = pt[in_off[i], + lens[i]),
+ * key keys[32 key_index[i]], sequence number seq[i] (TLS nonce and AD). */
+void so_tag_fold_mixed(const uint8_t* keys, const uint32_t* key_index, const uint64_t* seq, const uint32_t* lens,
+                       const uint64_t* in_off, const uint8_t* pt, size_t count, int threads, uint8_t out[16]);
+
+#ifdef __cplusplus
+}
+#endif
 
 #endif

@@ -65,6 +65,7 @@ class Oracle:
         L.so_open_batch_tls.restype = C.c_size_t
         L.so_tag_fold_tls.argtypes = [u8p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_size_t, C.c_size_t, C.c_int,
                                       C.c_void_p]
+        L.so_tag_fold_mixed.argtypes = [C.c_void_p] * 6 + [C.c_size_t, C.c_int, C.c_void_p]
         self.L = L
 
     # --- primitives
@@ -121,6 +122,20 @@ class Oracle:
         st = C.create_string_buffer(max(count, 1))
         bad = self.L.so_open_batch_tls(key, seq0, ct, n, count, out, st, threads)
         return bad, out.raw[:n * count], st.raw[:count]
+
+    def tag_fold_mixed(self, keys: bytes, key_index, seq, lens, in_off, pt, threads: int = 1) -> bytes:
+        """XOR of the tags of a mixed TLS batch (numpy uint32/uint64 arrays, pt a
+        uint8 numpy array): record i = pt[in_off[i]:+lens[i]], key key_index[i],
+        sequence number seq[i]."""
+        import numpy as np
+
+        arrs = [np.ascontiguousarray(a) for a in (key_index.astype(np.uint32), seq.astype(np.uint64),
+                                                  lens.astype(np.uint32), in_off.astype(np.uint64))]
+        kb = C.create_string_buffer(bytes(keys), len(keys))
+        out = C.create_string_buffer(16)
+        self.L.so_tag_fold_mixed(kb, *[a.ctypes.data_as(C.c_void_p) for a in arrs],
+                                 np.ascontiguousarray(pt).ctypes.data_as(C.c_void_p), len(lens), threads, out)
+        return out.raw
 
     def tag_fold_tls(self, key: bytes, seq0: int, seed: int, j0: int, n: int, count: int, threads: int = 1) -> bytes:
         """XOR of the tags of count sealed fill-rule records (never materialised)."""

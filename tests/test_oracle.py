@@ -184,3 +184,25 @@ def test_openssl_comparison_line_matches_oracle(oracle):
             t = bytearray(ct)
             t[-1] ^= 1
             assert ossl.open_batch_tls(key, 0xFFFFFFFE, bytes(t), n, count)[0] == 1
+
+
+def test_tag_fold_mixed_equals_per_record_seals(oracle):
+    """The full-size C2 checker of bench.py (so_tag_fold_mixed) folds exactly
+    the tags the per-record seal gives (TLS nonce/AD, per-connection keys)."""
+    import struct
+
+    import numpy as np
+
+    from suruga_amd import workloads as W
+
+    lay = W.c2_layout(300)
+    pt = np.frombuffer(np.random.default_rng(2).bytes(lay.pt_bytes), dtype=np.uint8)
+    seqs = lay.seq + np.uint64(7)
+    fold = oracle.tag_fold_mixed(lay.keys, lay.key_index, seqs, lay.lens, lay.in_off, pt, threads=4)
+    acc = bytearray(16)
+    for i in range(lay.count):
+        k = lay.keys[32 * int(lay.key_index[i]):32 * int(lay.key_index[i]) + 32]
+        s, n, o = int(seqs[i]), int(lay.lens[i]), int(lay.in_off[i])
+        tag = oracle.seal(k, struct.pack(">Q", s), pt[o:o + n].tobytes(), oracle.tls_ad(s, n))[-16:]
+        acc = bytearray(a ^ b for a, b in zip(acc, tag))
+    assert fold == bytes(acc)
