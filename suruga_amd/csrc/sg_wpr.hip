@@ -674,11 +674,26 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
             d[4] = ((v.v4 >> 24) + 0x80u + c) ^ 0x80u;
             uint8_t* ln = lines + kWprLineBytes * lane;
             const u32x4 z = zero4();
-            st16(ln, z);
-            st16(ln + 16, z);
-            st16(ln + 32, z);
+            if constexpr (TLS) {
+                // sigma = 5: line byte b = digit 42 - b (b = 26..42), i.e. the
+                // byte-reversed digit words R[k] = bswap(d[4 - k]) (digits 19 - 4k
+                // .. 16 - 4k, 17..19 zero) laid from byte 23 on: three 16-byte
+                // stores instead of 17 byte stores
+                uint32_t R[5];
 #pragma unroll
-            for (uint32_t i = 0; i < 17u; ++i) ln[47u - sigma - i] = (uint8_t)(d[i >> 2] >> (8u * (i & 3u)));
+                for (int k = 0; k < 5; ++k) R[k] = __builtin_bswap32(d[4 - k]);
+                st16(ln, z);
+                st16(ln + 16, u32x4{0u, R[0] << 24, __builtin_amdgcn_alignbyte(R[1], R[0], 1),
+                                    __builtin_amdgcn_alignbyte(R[2], R[1], 1)});
+                st16(ln + 32, u32x4{__builtin_amdgcn_alignbyte(R[3], R[2], 1), __builtin_amdgcn_alignbyte(R[4], R[3], 1),
+                                    R[4] >> 8, 0u});
+            } else {
+                st16(ln, z);
+                st16(ln + 16, z);
+                st16(ln + 32, z);
+#pragma unroll
+                for (uint32_t i = 0; i < 17u; ++i) ln[47u - sigma - i] = (uint8_t)(d[i >> 2] >> (8u * (i & 3u)));
+            }
         } else if (lane == kWprLines) {
             st16(lines + kWprLines * kWprLineBytes, zero4());
         }
