@@ -664,7 +664,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
         }
         wave_lds_sync();  // every table read is done before the lines overwrite it
         if (lane < kWprLines) {
-            const F26 v = canonical(lv);
+            // any representative below 2^130 of r^e works (the MAC is exact mod p):
+            // the carry ripple suffices, no conditional subtraction of p
+            const F26 v = ripple_full(lv);
             uint32_t c;  // digits = the bytes of v + 0x80..80, each ^ 0x80
             uint32_t d[5];
             d[0] = addc(v.v0 | (v.v1 << 26), 0x80808080u, 0u, &c) ^ 0x80808080u;
@@ -1160,7 +1162,7 @@ int set_wpr(int enable) {
 }
 
 const char* wpr_kernel_config() {
-    return "sg_wpr_kernel v14: full 16 KiB records, one wave per record (8 per 512-thread workgroup, persistent "
+    return "sg_wpr_kernel v15: full 16 KiB records, one wave per record (8 per 512-thread workgroup, persistent "
            "2 per CU, record groups handed out by a device counter), 4 KiB chunks LDS-DMA prefetched lane-contiguously into an XOR-swizzled LDS slice, output "
            "read out during the next chunk's first double rounds, lock-step grouped ChaCha20 rounds (s_barrier per "
            "rotate group; the first double round takes its uniform words from SGPRs, the counter-free steps once "
