@@ -314,7 +314,9 @@ def main():
         count, seq0 = hi - lo, lo
     else:            # weak scaling (the metric's mode): --records per rank, seq r*records + i
         count, seq0 = args.records, rank * args.records
-    stream = torch.cuda.current_stream(dev)
+    # the batch calls run asynchronously on a stream of their own: on the NULL
+    # (default) stream every call would end with a device sync (suruga_gpu.h)
+    stream = torch.cuda.Stream(dev)
     ws = torch.empty(B.workspace_size(count), dtype=torch.uint8, device=dev)
     status = torch.empty(count, dtype=torch.uint8, device=dev)
     if args.workload == "c1":
@@ -367,6 +369,7 @@ def main():
         B.N.check(lib.sg_seal_batch(C.byref(seal_c)))
         B.N.check(lib.sg_open_batch(C.byref(open_c)))
 
+    torch.cuda.synchronize()  # inputs and tables made on the default stream
     for _ in range(args.warmup):
         step()
     elapsed = shard.timed(dist, step, args.steps, sync=torch.cuda.synchronize,
@@ -376,6 +379,7 @@ def main():
     # round-trips, and (C1) every tag and a sample of records equal the oracle's
     mism = torch.zeros(1, dtype=torch.int64, device=dev)
     B.compare_records(*cmp_args, mism, stream=stream)
+    torch.cuda.synchronize()
     bad_status = int((status != 0).sum().item())
     roundtrip_ok = int(mism.item()) == 0 and bad_status == 0
     exact = None

@@ -749,7 +749,9 @@ hipError_t launch_aead_t(const KParams& p, uint32_t max_n, bool uniform, hipStre
     }
     uint32_t* const tail = ws_tail(p.ws, p.count);
     uint32_t* const lists = p.ws + (uint64_t)p.count * kWsLists;
-    if ((e = hipMemsetAsync(tail, 0, (kNumLists + 1u) * sizeof(uint32_t), s)) != hipSuccess) return e;
+    // populations, over-long count and the bucket group counters (the keying
+    // kernel resets the latter again): one dword fill
+    if ((e = hipMemsetD32Async((hipDeviceptr_t)tail, 0, kWsTailWords, s)) != hipSuccess) return e;
     const uint32_t per_wg = kClassifyThreads * kClassifyPerThread;
     hipLaunchKernelGGL(sg_classify_kernel<OPEN>, dim3((p.count + per_wg - 1u) / per_wg), dim3(kClassifyThreads), 0, s,
                        p, lists, tail, max_n);
@@ -760,13 +762,18 @@ hipError_t launch_aead_t(const KParams& p, uint32_t max_n, bool uniform, hipStre
     // record is keyed and the classes run on persistent grids instead (and the
     // caller leaves p.wpr_mix off: the wave-per-record buckets need their
     // populations).
+    // (into pinned memory of the calling thread: a DMA, no staging copy)
+    thread_local uint32_t* pop_pinned = nullptr;
     uint32_t pop[kNumLists + 1];
     hipStreamCaptureStatus cap_status = hipStreamCaptureStatusNone;
     if ((e = hipStreamIsCapturing(s, &cap_status)) != hipSuccess) return e;
     const bool exact = cap_status == hipStreamCaptureStatusNone;
     if (exact) {
-        if ((e = hipMemcpyAsync(pop, tail, sizeof pop, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+        if (!pop_pinned && (e = hipHostMalloc((void**)&pop_pinned, sizeof pop, hipHostMallocDefault)) != hipSuccess)
+            return e;
+        if ((e = hipMemcpyAsync(pop_pinned, tail, sizeof pop, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
         if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+        for (uint32_t i = 0; i <= kNumLists; ++i) pop[i] = pop_pinned[i];
         *over = pop[kTailOver];
         // size-class keying over the class lists only
         KeyJobs jobs = {};
