@@ -311,12 +311,18 @@ __global__ __launch_bounds__(kPackThreads) void sg_pack_kernel(const KParams p, 
         const uint32_t ctr = j + 1u, n14 = sl[kSN14], n15 = sl[kSN15];  // data uses blocks 1.. (chacha20_poly1305.rs:52)
         uint32_t x[16] = {kSigma0, kSigma1, kSigma2, kSigma3, kw[0], kw[1], kw[2], kw[3],
                           kw[4],   kw[5],   kw[6],   kw[7],   ctr,     0u,    n14,   n15};
+        // EXEC limited to the lanes with a block (none in a round without a
+        // chunk for this wave; s_barrier ignores EXEC, so all waves still meet)
+        const uint64_t live = __builtin_amdgcn_ballot_w64(valid);
 #pragma unroll
         for (int dr = 0; dr < 10; ++dr) {
-            asm volatile(SG_CHACHA_DR_NB1_BAR1
+            uint64_t sv;
+            asm volatile("s_and_saveexec_b64 %16, %17\n" SG_CHACHA_DR_NB1_BAR1 "s_mov_b64 exec, %16\n"
                          : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]),
                            "+v"(x[7]), "+v"(x[8]), "+v"(x[9]), "+v"(x[10]), "+v"(x[11]), "+v"(x[12]), "+v"(x[13]),
-                           "+v"(x[14]), "+v"(x[15]));
+                           "+v"(x[14]), "+v"(x[15]), "=&s"(sv)
+                         : "s"(live)
+                         : "scc");
         }
         if (valid) {
             // feed-forward (chacha20.rs:104-106) and XOR (chacha20.rs:143-153)
@@ -420,7 +426,7 @@ int set_pack(int enable) {
 }
 
 const char* pack_kernel_config() {
-    return "sg_pack_kernel v2: mixed-batch TLS records of 64 B-4 KiB (multiples of 64 B) packed 64-byte block per lane "
+    return "sg_pack_kernel v3: mixed-batch TLS records of 64 B-4 KiB (multiples of 64 B) packed 64-byte block per lane "
            "across 128-record runs (512-thread workgroups, chunk rounds, lock-step grouped ChaCha20 rounds), keying in the same kernel "
            "(block 0, r^(1+32a) and r^(4b) tables in LDS), per-lane Poly1305 share as a 4-step radix-2^32 Horner times "
            "r^(1+4i), LDS atomic accumulation, constant term for AD / length / pads";

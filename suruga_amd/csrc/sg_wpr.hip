@@ -608,6 +608,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
         const uint32_t n = LIST ? cd.n : kWprN;
         const uint32_t vs = kWprN - n;                             // frame offset of the record
         const uint32_t lo = LIST ? kWprChunk * J - n : 0u;         // idle bytes of chunk j0
+        // the lanes of chunk j0 that hold record bytes (the others sit out its rounds)
+        const uint64_t live0 = LIST ? __builtin_amdgcn_ballot_w64(64u * lane >= lo) : ~0ull;
         const uint8_t* inb = p.in + cd.io;
         uint8_t* outb = p.out + cd.oo;
         uint32_t gn = ngroups, gnn = ngroups;  // the next group (uniform launches: known from iteration 3 on)
@@ -781,6 +783,18 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
                    "+v"(x[8]), "+v"(x[9]), "+v"(x[10]), "+v"(x[11]), "+v"(x[12]), "+v"(x[13]), "+v"(x[14]),         \
                    "+v"(x[15]))
 #define SG_PIN() __builtin_amdgcn_sched_barrier(0)
+    // chunk j0 of a shorter record: the double rounds run with EXEC limited to
+    // its live lanes (restored in the same statement; s_barrier ignores EXEC)
+#define SG_DR_LIVE()                                                                                              \
+    do {                                                                                                          \
+        uint64_t sv;                                                                                              \
+        asm volatile("s_and_saveexec_b64 %16, %17\n" SG_WPR_DR_ASM "s_mov_b64 exec, %16\n"                       \
+                     : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]),          \
+                       "+v"(x[7]), "+v"(x[8]), "+v"(x[9]), "+v"(x[10]), "+v"(x[11]), "+v"(x[12]), "+v"(x[13]),       \
+                       "+v"(x[14]), "+v"(x[15]), "=&s"(sv)                                                          \
+                     : "s"(live0)                                                                                 \
+                     : "scc");                                                                                    \
+    } while (0)
 
 #pragma unroll
         for (uint32_t j = j0; j < 4u; ++j) {
@@ -817,14 +831,19 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
             u32x4 D[4];
             SG_PIN();
             // first double round: every word but the counter enters from SGPRs
-            asm volatile(SG_CHACHA_DR1S_COL : "=v"(x[0]), "=v"(x[4]), "=v"(x[8]), "+v"(x[12])
-                         : "s"(S0), "s"(kw[0]), "s"(kw[4]));
-            asm volatile(SG_CHACHA_DR1S_DIAG
+            // (EXEC limited to the live lanes in chunk j0 of a shorter record; the
+            // rounds run at full EXEC, restored at the end of each statement, and
+            // the live mask is the last operand so that the macros' numbering holds)
+            const uint64_t live = (LIST && j == j0) ? live0 : ~0ull;
+            asm volatile("s_mov_b64 exec, %7\n" SG_CHACHA_DR1S_COL "s_mov_b64 exec, -1\n"
+                         : "=v"(x[0]), "=v"(x[4]), "=v"(x[8]), "+v"(x[12])
+                         : "s"(S0), "s"(kw[0]), "s"(kw[4]), "s"(live));
+            asm volatile("s_mov_b64 exec, %28\n" SG_CHACHA_DR1S_DIAG "s_mov_b64 exec, -1\n"
                          : "+v"(x[0]), "+v"(x[4]), "+v"(x[8]), "+v"(x[12]), "=v"(x[1]), "=v"(x[2]), "=v"(x[3]),
                            "=v"(x[5]), "=v"(x[6]), "=v"(x[7]), "=v"(x[9]), "=v"(x[10]), "=v"(x[11]), "=v"(x[13]),
                            "=v"(x[14]), "=v"(x[15])
                          : "s"(u[5]), "s"(u[15]), "s"(T1), "s"(u[3]), "s"(u[14]), "s"(u[10]), "s"(u[11]), "s"(T13),
-                           "s"(u[9]), "s"(u[6]), "s"(u[7]), "s"(T2));
+                           "s"(u[9]), "s"(u[6]), "s"(u[7]), "s"(T2), "s"(live));
             SG_PIN();
             // The previous chunk's output leaves lane-contiguously one 1 KiB piece
             // per double round (read from LDS one gap ahead of its store), and
@@ -848,7 +867,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
             if (j > j0) mac_load(j - 1u, 0u, R0);
             if (pend) oa = out_piece(0u);
             SG_PIN();
-            SG_DR();
+            if (LIST && j == j0) SG_DR_LIVE(); else SG_DR();
             SG_PIN();
             if (LIST && j == 3u) {  // wave 0 published it at the start of iteration j0 + 1 (LIST: J >= 2)
                 gnn = uniform(*gslot);
@@ -862,7 +881,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
                 ob = out_piece(1u);
             }
             SG_PIN();
-            SG_DR();
+            if (LIST && j == j0) SG_DR_LIVE(); else SG_DR();
             SG_PIN();
             if (j > j0) {
                 mac_mfma(R1, A[1]);
@@ -874,7 +893,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
             }
             dma_piece(0u);
             SG_PIN();
-            SG_DR();
+            if (LIST && j == j0) SG_DR_LIVE(); else SG_DR();
             SG_PIN();
             if (j > j0) {
                 mac_mfma(R0, A[2]);
@@ -886,13 +905,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
             }
             dma_piece(1u);
             SG_PIN();
-            SG_DR();
+            if (LIST && j == j0) SG_DR_LIVE(); else SG_DR();
             SG_PIN();
             if (j > j0) mac_mfma(R1, A[3]);
             if (pend) store_piece(3u, ob);
             dma_piece(2u);
             SG_PIN();
-            SG_DR();
+            if (LIST && j == j0) SG_DR_LIVE(); else SG_DR();
             SG_PIN();
             dma_piece(3u);
             if (j == 3u) {
@@ -900,7 +919,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
                 mac_load(3u, 1u, R1);
             }
             SG_PIN();
-            SG_DR();
+            if (LIST && j == j0) SG_DR_LIVE(); else SG_DR();
             SG_PIN();
             if (j == 3u) {
                 F3[0] = mac_frag(R0);
@@ -909,19 +928,19 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
                 mac_load(3u, 3u, R1);
             }
             SG_PIN();
-            SG_DR();
+            if (LIST && j == j0) SG_DR_LIVE(); else SG_DR();
             SG_PIN();
             if (j == 3u) {
                 F3[2] = mac_frag(R0);
                 F3[3] = mac_frag(R1);
             }
             SG_PIN();
-            SG_DR();
+            if (LIST && j == j0) SG_DR_LIVE(); else SG_DR();
             SG_PIN();
 #pragma unroll
             for (uint32_t i = 0; i < 4u; ++i) D[i] = ld16(cb + 16u * (4u * lane + (i ^ xq)));
             SG_PIN();
-            SG_DR();
+            if (LIST && j == j0) SG_DR_LIVE(); else SG_DR();
             SG_PIN();
             SG_TICK(t_jr);
             SG_ACC(3, t_jw, t_jr);  // rounds (+ MAC of the previous chunk)
@@ -1162,14 +1181,15 @@ int set_wpr(int enable) {
 }
 
 const char* wpr_kernel_config() {
-    return "sg_wpr_kernel v15: full 16 KiB records, one wave per record (8 per 512-thread workgroup, persistent "
+    return "sg_wpr_kernel v16: full 16 KiB records, one wave per record (8 per 512-thread workgroup, persistent "
            "2 per CU, record groups handed out by a device counter), 4 KiB chunks LDS-DMA prefetched lane-contiguously into an XOR-swizzled LDS slice, output "
            "read out during the next chunk's first double rounds, lock-step grouped ChaCha20 rounds (s_barrier per "
            "rotate group; the first double round takes its uniform words from SGPRs, the counter-free steps once "
            "per record on the SALU), Poly1305 as 16 "
            "v_mfma_i32_32x32x32_i8 per record fed from the ciphertext registers one chunk behind (Toeplitz digit "
            "lines of r^(128k+d) in LDS, read as aligned dwords + v_alignbyte), exact per-lane assembly, "
-           "W = r^(4(31-q)) scaling, DPP sum; keying pre-pass with the constant term";
+           "W = r^(4(31-q)) scaling, DPP sum; keying pre-pass with the constant term; bucket records: the idle lanes "
+           "of the first chunk sit out its rounds (EXEC)";
 }
 
 }  // namespace sg
