@@ -14,7 +14,9 @@
 // idles except in the run's last chunk and the last round.  The eight waves
 // run the rounds in lock-step (grouped ARX asm with an s_barrier per rotate
 // group, sg_chacha_grp.inc, as the wave-per-record kernel): the two waves of
-// a SIMD then issue their full-rate add / xor back to back.
+// a SIMD then issue their full-rate add / xor back to back.  Lanes without a
+// block (a round with no chunk for the wave, the tail of the last chunk) run
+// the rounds with EXEC off, which saves power (the launch is power-capped).
 //
 //   setup (waves 0-1, one lane per record): keystream block 0 -> r, s
 //     (chacha20_poly1305.rs:50-52, poly1305.rs:197-203), the powers
@@ -427,7 +429,8 @@ int set_pack(int enable) {
 
 const char* pack_kernel_config() {
     return "sg_pack_kernel v3: mixed-batch TLS records of 64 B-4 KiB (multiples of 64 B) packed 64-byte block per lane "
-           "across 128-record runs (512-thread workgroups, chunk rounds, lock-step grouped ChaCha20 rounds), keying in the same kernel "
+           "across 128-record runs (512-thread workgroups, chunk rounds, lock-step grouped ChaCha20 rounds with EXEC limited "
+           "to the lanes holding a block), keying in the same kernel "
            "(block 0, r^(1+32a) and r^(4b) tables in LDS), per-lane Poly1305 share as a 4-step radix-2^32 Horner times "
            "r^(1+4i), LDS atomic accumulation, constant term for AD / length / pads";
 }
