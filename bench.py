@@ -11,6 +11,9 @@ bytes processed by seal and open on all ranks / wall time of the timed region
 
 Usage:  python bench.py [--gpus N] [--steps K] [--warmup W]
         torchrun --nproc-per-node N bench.py --gpus N ...   (N > 1)
+With --gpus N > 1 and no launcher environment (WORLD_SIZE unset) bench.py
+starts the N rank processes itself (one per GPU, 127.0.0.1 rendezvous)
+before anything touches a GPU, and exits with the worst rank's code.
 """
 from __future__ import annotations
 
@@ -43,8 +46,9 @@ def parse():
                     help="c1: 16 KiB records, one key (the metric's config); c2: Zipf 64 B-16 KiB, 256 keys")
     ap.add_argument("--records", type=int, default=1 << 20, help="records per GPU (C1: 2^20)")
     ap.add_argument("--record-bytes", type=int, default=16384)
-    ap.add_argument("--cpu-sample", type=int, default=4096, help="records in the CPU-baseline sample")
-    ap.add_argument("--cpu-seconds", type=float, default=2.0, help="min wall time of the CPU baseline")
+    ap.add_argument("--cpu-per-thread", type=int, default=64,
+                    help="CPU baseline: records per thread in the sample (C2: 8x as many)")
+    ap.add_argument("--cpu-seconds", type=float, default=2.5, help="min wall time of each CPU-baseline line")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-bitexact", action="store_true",
                     help="skip the oracle tag fold / sample compare of the last step (C1 and C2)")
@@ -57,11 +61,45 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(args, n):
+def cpu_quota():
+    """CPUs this process may use per the cgroup CPU quota (None: unlimited).
+    On the GPU box the affinity mask lists every CPU of the host while the
+    container is granted a share of them; threads beyond the share only
+    time-slice (round 2's 256-thread baseline ran on a ~16-CPU share)."""
+    for path, parse in (("/sys/fs/cgroup/cpu.max", lambda t: t.split()[:2]),
+                        ("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", None)):
+        try:
+            if parse:
+                q, per = parse(open(path).read())
+                if q != "max":
+                    return float(q) / float(per)
+            else:
+                q = int(open(path).read())
+                per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+                if q > 0:
+                    return q / per
+        except (OSError, ValueError):
+            continue
+    return None
+
+
+def host_cpus():
+    """(threads to use, affinity-mask CPUs, cgroup quota in CPUs or None)."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = cpu_quota()
+    use = aff if quota is None else max(1, min(aff, int(quota + 0.999)))
+    return use, aff, quota
+
+
+def cpu_baseline(args, n, lay=None):
     """CPU lines on the host cores, bounded samples; only the C calls are timed
     (buffers preallocated).  kind "port": the oracle (the reference's scalar
     algorithm restated in C); optimised_cpu: the same AEAD composed from
-    OpenSSL's vectorised ChaCha20 / Poly1305 (SURVEY.md 8d's optional line)."""
+    OpenSSL's vectorised ChaCha20 / Poly1305 (SURVEY.md 8d's optional line).
+    Both run on a persistent thread pool (oracle/so_pool.h), one contiguous
+    slice of >= --cpu-per-thread records per thread, on the CPUs the cgroup
+    quota grants (host_cpus).  C1: uniform 16 KiB TLS records; C2 (lay): the
+    first records of the same Zipf layout with their connection keys."""
     import ctypes as C
 
     import numpy as np
@@ -71,15 +109,36 @@ def cpu_baseline(args, n):
     from oracle_ffi import oracle as get_oracle
 
     o = get_oracle()
-    count = args.cpu_sample
-    threads = host_threads()
-    pt = np.empty(count * n, dtype=np.uint8)
-    ct = np.empty(count * (n + 16), dtype=np.uint8)
-    back = np.empty(count * n, dtype=np.uint8)
-    st = np.empty(count, dtype=np.uint8)
+    threads, aff, quota = host_cpus()
     ptr = lambda a, off=0: C.c_void_p(a.ctypes.data + off)  # noqa: E731
-    for j in range(count):
-        o.L.so_fill_record(SEED, j, ptr(pt, j * n), n)
+    if lay is None:
+        count = max(args.cpu_per_thread * threads, 64)
+        pt = np.empty(count * n, dtype=np.uint8)
+        ct = np.empty(count * (n + 16), dtype=np.uint8)
+        back = np.empty(count * n, dtype=np.uint8)
+        for j in range(count):
+            o.L.so_fill_record(SEED, j, ptr(pt, j * n), n)
+        rec_bytes = lambda recs: recs * n  # noqa: E731
+        desc = f"{n} B TLS records"
+    else:
+        # the first records of the C2 layout, whose mean record is ~2 KiB:
+        # 8x the records per thread for a comparable slice of bytes
+        count = min(lay.count, max(8 * args.cpu_per_thread * threads, 512))
+        lens = np.ascontiguousarray(lay.lens[:count].astype(np.uint32))
+        olens = np.ascontiguousarray(lens + np.uint32(16))
+        io = np.ascontiguousarray(lay.in_off[:count].astype(np.uint64))
+        oo = np.ascontiguousarray(lay.out_off[:count].astype(np.uint64))
+        ki = np.ascontiguousarray(lay.key_index[:count].astype(np.uint32))
+        sq = np.ascontiguousarray(lay.seq[:count].astype(np.uint64))
+        kb = np.frombuffer(bytes(lay.keys), dtype=np.uint8).copy()
+        pt_bytes = int(io[-1]) + int(lens[-1]) + 64
+        pt = np.frombuffer(np.random.default_rng(SEED).bytes(pt_bytes), dtype=np.uint8).copy()
+        ct = np.empty(int(oo[-1]) + int(lens[-1]) + 16 + 64, dtype=np.uint8)
+        back = np.empty(pt_bytes, dtype=np.uint8)
+        csum = np.concatenate([[0], np.cumsum(lens.astype(np.int64))])
+        rec_bytes = lambda recs: int(csum[recs])  # noqa: E731
+        desc = f"C2 Zipf TLS records (mean {csum[-1] / count:.0f} B), 256 connection keys"
+    st = np.empty(count, dtype=np.uint8)
 
     def timed(seal, open_, recs, thr):
         reps, t = 0, 0.0
@@ -90,17 +149,32 @@ def cpu_baseline(args, n):
             t += time.perf_counter() - t0
             reps += 1
             assert bad == 0
-        assert np.array_equal(back[:recs * n], pt[:recs * n])
-        return 2 * recs * n * reps / t / 2**30, reps
+        m = rec_bytes(recs) if lay is None else int(io[recs - 1]) + int(lens[recs - 1])
+        if lay is None:
+            assert np.array_equal(back[:m], pt[:m])
+        else:
+            assert all(np.array_equal(back[int(io[i]):int(io[i]) + int(lens[i])], pt[int(io[i]):int(io[i]) + int(lens[i])])
+                       for i in range(0, recs, max(1, recs // 64)))
+        return 2 * rec_bytes(recs) * reps / t / 2**30, reps
 
-    def o_seal(recs, thr):
-        o.L.so_seal_batch_tls(KEY, 0, ptr(pt), n, recs, ptr(ct), thr)
+    if lay is None:
+        def o_seal(recs, thr):
+            o.L.so_seal_batch_tls(KEY, 0, ptr(pt), n, recs, ptr(ct), thr)
 
-    def o_open(recs, thr):
-        return o.L.so_open_batch_tls(KEY, 0, ptr(ct), n, recs, ptr(back), ptr(st), thr)
+        def o_open(recs, thr):
+            return o.L.so_open_batch_tls(KEY, 0, ptr(ct), n, recs, ptr(back), ptr(st), thr)
+    else:
+        def o_seal(recs, thr):
+            o.L.so_batch_mixed(0, ptr(kb), ptr(ki), ptr(sq), ptr(lens), ptr(io), ptr(oo), ptr(pt), ptr(ct), None,
+                               recs, thr)
 
+        def o_open(recs, thr):
+            return o.L.so_batch_mixed(1, ptr(kb), ptr(ki), ptr(sq), ptr(olens), ptr(oo), ptr(io), ptr(ct),
+                                      ptr(back), ptr(st), recs, thr)
+
+    one_recs = max(16, count // threads)  # one thread's slice of the multi-thread run
     gibs, reps = timed(o_seal, o_open, count, threads)
-    one, _ = timed(o_seal, o_open, max(64, count // 16), 1)  # the reference is single-threaded per connection
+    one, _ = timed(o_seal, o_open, one_recs, 1)  # the reference is single-threaded per connection
     model = ""
     try:
         for line in open("/proc/cpuinfo"):
@@ -111,38 +185,47 @@ def cpu_baseline(args, n):
         pass
     try:
         L = OsslLine().L
+        if lay is None:
+            def s_seal(recs, thr):
+                L.ossl_batch_tls(0, KEY, 0, ptr(pt), n, recs, ptr(ct), thr)
 
-        def s_seal(recs, thr):
-            L.ossl_batch_tls(0, KEY, 0, ptr(pt), n, recs, ptr(ct), thr)
+            def s_open(recs, thr):
+                return L.ossl_batch_tls(1, KEY, 0, ptr(ct), n, recs, ptr(back), thr)
+        else:
+            def s_seal(recs, thr):
+                L.ossl_batch_mixed(0, ptr(kb), ptr(ki), ptr(sq), ptr(lens), ptr(io), ptr(oo), ptr(pt), ptr(ct),
+                                   recs, thr)
 
-        def s_open(recs, thr):
-            return L.ossl_batch_tls(1, KEY, 0, ptr(ct), n, recs, ptr(back), thr)
+            def s_open(recs, thr):
+                return L.ossl_batch_mixed(1, ptr(kb), ptr(ki), ptr(sq), ptr(olens), ptr(oo), ptr(io), ptr(ct),
+                                          ptr(back), recs, thr)
 
         og, oreps = timed(s_seal, s_open, count, threads)
-        o1, _ = timed(s_seal, s_open, max(64, count // 16), 1)
+        o1, _ = timed(s_seal, s_open, one_recs, 1)
         ossl = {"value": round(og, 3), "unit": "GiB/s", "cores": threads, "single_thread_gibs": round(o1, 4),
-                "impl": "OpenSSL libcrypto EVP_chacha20 + EVP_MAC POLY1305 composed per suruga's AEAD "
-                        "(oracle/ossl_aead.c)",
-                "sample": f"{count} x {n} B TLS records seal+open, x{oreps} repetitions"}
+                "scaling_efficiency": round(og / (o1 * threads), 3),
+                "impl": "OpenSSL libcrypto ChaCha20 + EVP_MAC POLY1305 (fetched once, one context pair per thread) "
+                        "composed per suruga's AEAD (oracle/ossl_aead.c)",
+                "sample": f"{count} x {desc} seal+open, x{oreps} repetitions"}
     except (OSError, AssertionError) as e:
         ossl = {"unavailable": str(e)}
     return {
         "value": round(gibs, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
-        "sample": f"{count} x {n} B TLS records seal+open, x{reps} repetitions, {threads} threads "
+        "sample": f"{count} x {desc} seal+open, x{reps} repetitions, {threads} threads on a persistent pool "
                   f"(oracle/suruga_oracle.c, the reference's scalar algorithm)",
-        "single_thread_gibs": round(one, 4), "cpu": model or platform.processor(),
-        "host_logical_cpus": os.cpu_count(),
-        "cores_note": "threads = every CPU in this process's affinity mask (os.sched_getaffinity); "
-                      "host_logical_cpus = all logical CPUs of the machine",
+        "single_thread_gibs": round(one, 4),
+        "scaling_efficiency": round(gibs / (one * threads), 3),
+        "cpu": model or platform.processor(),
+        "affinity_cpus": aff, "cgroup_cpu_quota": quota, "host_logical_cpus": os.cpu_count(),
+        "cores_note": "threads = the CPUs the cgroup quota grants (affinity_cpus if unlimited); "
+                      "scaling_efficiency = value / (single_thread_gibs x cores)",
         "optimised_cpu": ossl,
     }
 
 
 def host_threads() -> int:
-    """Every CPU this process may run on (the box's CPU share), uncapped."""
-    if hasattr(os, "sched_getaffinity"):
-        return max(1, len(os.sched_getaffinity(0)))
-    return max(1, os.cpu_count() or 1)
+    """Threads for the oracle checkers: the CPUs this process may use."""
+    return host_cpus()[0]
 
 
 def bitexact_check(ct, n, count, seq0):
@@ -278,8 +361,60 @@ def sum_over_ranks(dist, value, device=None):
     return float(t.item())
 
 
+def launch_ranks(args):
+    """--gpus N without a launcher: start the N rank processes here, one per
+    GPU (LOCAL_RANK r), with a 127.0.0.1 rendezvous, before this process makes
+    any GPU call; wait for all of them and return the worst exit code (None:
+    this process is itself a rank).  A rank that fails ends the others (its
+    peers would wait at the next barrier forever)."""
+    import signal
+    import socket
+    import subprocess
+
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != args.gpus:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher set WORLD_SIZE={ws}")
+        return None
+    if args.gpus <= 1:
+        return None
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve()), *sys.argv[1:]], env=env))
+    rcs = [None] * len(procs)
+    while any(rc is None for rc in rcs):
+        for i, pr in enumerate(procs):
+            if rcs[i] is None:
+                rcs[i] = pr.poll()
+        if any(rc not in (None, 0) for rc in rcs):
+            for i, pr in enumerate(procs):  # the ranks this process started, by PID
+                if rcs[i] is None:
+                    pr.send_signal(signal.SIGTERM)
+            for i, pr in enumerate(procs):
+                if rcs[i] is None:
+                    try:
+                        rcs[i] = pr.wait(timeout=30)
+                    except subprocess.TimeoutExpired:
+                        pr.kill()
+                        rcs[i] = pr.wait()
+            break
+        time.sleep(0.05)
+    bad = [rc for rc in rcs if rc != 0]
+    if bad:
+        print(f"bench.py: rank exit codes {rcs}", file=sys.stderr, flush=True)
+    return bad[0] if bad else 0
+
+
 def main():
     args = parse()
+    rc = launch_ranks(args)
+    if rc is not None:
+        sys.exit(rc)
     import torch
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -331,6 +466,7 @@ def main():
                          out_stride=n, seq0=seq0, status=status, workspace=ws, stream=stream)
         payload_per_step = 2 * count * n
         alg = {"seal": (2 * n + 69) * count, "open": (2 * n + 70) * count}
+        alg_read = {"seal": (n + 53) * count, "open": (n + 69) * count}  # R alone: pt|ct(+tag) + ad + nonce + key
         cfg = {"workload": f"C1: {count} x {n} B TLS records per GPU, one key, sequential seq, seal then open, "
                            "device-resident", "records_per_gpu": count, "record_bytes": n}
         cmp_args = (pt, n, back, n, n, count)
@@ -357,6 +493,7 @@ def main():
                          out_off=in_off, key_index=kidx, seq=seqs, status=status, workspace=ws, stream=stream)
         payload_per_step = 2 * lay.payload
         alg = {"seal": 2 * lay.payload + 69 * count, "open": 2 * lay.payload + 70 * count}
+        alg_read = {"seal": lay.payload + 53 * count, "open": lay.payload + 69 * count}
         cfg = {"workload": f"C2: {count} TLS records per GPU, Zipf(1.1) sizes 64 B-16 KiB (mean "
                            f"{lay.payload / count:.0f} B), 256 connection keys, seal then open, device-resident",
                            "records_per_gpu": count, "record_bytes": "zipf"}
@@ -375,6 +512,15 @@ def main():
     elapsed = shard.timed(dist, step, args.steps, sync=torch.cuda.synchronize,
                           device=dev if backend == "nccl" else None)
 
+    # per-kernel device time with HIP events on the launch stream, right after
+    # the timed steps while the GPU is still at its steady-state clock (round 2
+    # took them after the CPU oracle fold, on a GPU that had idled for seconds)
+    B.set_timing(True)
+    for _ in range(max(5, min(args.steps, 10))):
+        step()
+    tm = B.timing_read()
+    B.set_timing(False)
+
     # correctness of the last step (outside the timed region): every record
     # round-trips, and (C1) every tag and a sample of records equal the oracle's
     mism = torch.zeros(1, dtype=torch.int64, device=dev)
@@ -388,13 +534,6 @@ def main():
         exact = bitexact_check(ct, n, count, seq0) if args.workload == "c1" else \
             bitexact_check_c2(lay, pt, ct, seq0 // 256)
         roundtrip_ok = roundtrip_ok and exact["bitexact_fold"] and exact["bitexact_sample"]
-
-    # per-kernel device time with HIP events on the launch stream
-    B.set_timing(True)
-    for _ in range(5):
-        step()
-    tm = B.timing_read()
-    B.set_timing(False)
 
     scatter_gather = None
     if world > 1 and args.sg_records > 0 and args.workload == "c1":
@@ -417,6 +556,9 @@ def main():
     alg_bytes = alg[dom]
     dom_ms = tm[f"{dom}_ms"]
     achieved = alg_bytes / (dom_ms * 1e-3) / 1e9
+    achieved_read = alg_read[dom] / (dom_ms * 1e-3) / 1e9
+    # the event-timed kernels of one step against the wall-clock step
+    kernel_sum_ms = tm["seal_ms"] + tm["open_ms"] + 2 * tm["keying_ms"]
     traffic, valu, traffic_src = None, None, None
     # the PMC traffic summary of this exact kernel build and workload (the newest
     # profiles/traffic_*.json whose build string and record shape match)
@@ -461,8 +603,8 @@ def main():
                       "+ size classes (one batch)")
     if rank == 0:
         cpu = None
-        if world == 1 and not args.no_cpu_baseline and args.workload == "c1":
-            cpu = cpu_baseline(args, n)
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(args, n) if args.workload == "c1" else cpu_baseline(args, 0, lay)
         line = {
             "metric": METRIC, "value": round(value, 3), "unit": "GiB/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
@@ -472,10 +614,16 @@ def main():
             "roofline": {"bound": "hbm", "kernel": dom_kernel,
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
-                         "alg_bytes_per_launch": alg_bytes, "avg_launch_ms": round(dom_ms, 4)},
+                         "alg_bytes_per_launch": alg_bytes, "avg_launch_ms": round(dom_ms, 4),
+                         # SURVEY.md 8(d)'s read-only variant (the north star's "HBM-read roofline")
+                         "hbm_read": {"achieved": round(achieved_read, 1), "frac": round(achieved_read / HBM_PEAK_GBS, 4),
+                                      "alg_read_bytes_per_launch": alg_read[dom]}},
             "valu_roofline": valu,
             "kernel_ms": {"seal": round(tm["seal_ms"], 4), "open": round(tm["open_ms"], 4),
-                          "keying": round(tm["keying_ms"], 4)},
+                          "keying": round(tm["keying_ms"], 4), "sum_per_step": round(kernel_sum_ms, 4),
+                          "sum_vs_step": round(kernel_sum_ms / ms_per_step, 4),
+                          "launches": int(tm.get("n_seal", 0)) + int(tm.get("n_open", 0)),
+                          "note": "HIP events on the launch stream over steps run right after the timed region"},
             "records_per_s": round((args.records if args.strong else count * world) * args.steps / elapsed, 1),
             "correct": roundtrip_ok,
             "cpu_baseline": cpu,

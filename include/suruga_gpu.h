@@ -94,6 +94,12 @@ int sg_open(sg_ctx* ctx, const uint8_t* nonce, size_t nonce_len,
 #define SG_BATCH_TLS  0x1u  /* nonce = be64(seq_i); ad = be64(seq_i) || content_type ||
                                ver_major || ver_minor || be16(n_i)  (tls.rs:103-112,
                                250-265); `nonces`/`ads` are ignored               */
+#define SG_BATCH_KEEP_FAILED 0x2u  /* open: leave the (unauthenticated) plaintext of
+                                      records whose status is SG_E_BAD_MAC in `out`.
+                                      By default it is zero-filled after the batch, as
+                                      the reference hands out no plaintext with its
+                                      Err (chacha20_poly1305.rs:89-93; the decryption
+                                      itself always runs, :80-82).                   */
 
 typedef struct sg_batch {
     uint32_t count;            /* number of records                                 */
@@ -127,8 +133,9 @@ typedef struct sg_batch {
      *         SG_E_SHORT), output = plaintext (len_i - 16)
      * len_i = len ? len[i] : uniform_len.  max_len >= every len_i is required
      * when len != NULL (it sizes the LDS staging of one record); a longer
-     * record is skipped and the call returns SG_E_ARG (under stream capture it
-     * is skipped silently).                                                    */
+     * record is skipped and the call returns SG_E_ARG once every other record
+     * is done (on a NULL stream: after the device work has finished; under
+     * stream capture it is skipped silently).                                  */
     const uint8_t*  in;
     const uint64_t* in_off;
     uint64_t        in_stride;
@@ -140,7 +147,10 @@ typedef struct sg_batch {
     uint32_t        max_len;
 
     /* open: per-record status, device: SG_OK / SG_E_BAD_MAC / SG_E_SHORT, or
-     * SG_STATUS_SKIPPED for a record longer than max_len (not processed)    */
+     * SG_STATUS_SKIPPED for a record longer than max_len (not processed, its
+     * output left untouched).  The output of an SG_E_BAD_MAC record is zeroed
+     * unless flags has SG_BATCH_KEEP_FAILED: it is never authenticated
+     * plaintext.                                                             */
     uint8_t*        status;
 
     /* HIP stream (hipStream_t).  Non-NULL: the call is asynchronous on that
@@ -170,8 +180,10 @@ typedef struct sg_batch {
 size_t sg_workspace_size(uint32_t count);
 
 /* Batch seal / open on device-resident records.  Records are independent
- * (one workgroup each).  Returns SG_OK or < 0 for argument/HIP errors;
- * per-record MAC results of open land in b->status. */
+ * (one wave each for 4-16 KiB records, 64-byte blocks of many small records
+ * packed into one wave, or 2-256 lanes per record in the size classes).
+ * Returns SG_OK or < 0 for argument/HIP errors; per-record MAC results of
+ * open land in b->status. */
 int sg_seal_batch(const sg_batch* b);
 int sg_open_batch(const sg_batch* b);
 
@@ -270,6 +282,8 @@ int sg_compare_records(const uint8_t* a, uint64_t stride_a, const uint8_t* b,
 /* ---- diagnostics -------------------------------------------------------- */
 const char* sg_last_error(void);       /* thread-local message of the last failure */
 const char* sg_build_info(void);       /* arch + kernel configuration string       */
+const char* sg_source_hash(void);      /* hash of the sources the library was built
+                                          from (16 hex digits; suruga_amd/_build.py) */
 /* Kernel timing with HIP events recorded on the launch stream.  While timing
  * is enabled every batch call brackets its keying kernel and its seal/open
  * kernel with events; sg_timing_read synchronises on them and returns the

@@ -17,6 +17,8 @@
 #include <openssl/core_names.h>
 #include <openssl/evp.h>
 #include <pthread.h>
+
+#include "so_pool.h"
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -26,10 +28,15 @@ typedef struct {
     EVP_MAC_CTX* m;
 } ossl_ctx;
 
-static int ossl_init(ossl_ctx* x, EVP_MAC* mac) {
+/* The cipher and MAC are fetched once per batch call and every thread keeps
+ * one cipher and one MAC context for its whole slice, re-keyed per record
+ * with init only.  (Round 2 re-initialised with EVP_chacha20() per record: an
+ * implicit fetch on OpenSSL 3's global store whose lock serialised the
+ * threads, so the 256-thread line ran at the single-thread rate.) */
+static int ossl_init(ossl_ctx* x, EVP_CIPHER* cipher, EVP_MAC* mac) {
     x->c = EVP_CIPHER_CTX_new();
     x->m = EVP_MAC_CTX_new(mac);
-    return x->c && x->m;
+    return x->c && x->m && EVP_EncryptInit_ex2(x->c, cipher, NULL, NULL, NULL) == 1;
 }
 
 static void ossl_free(ossl_ctx* x) {
@@ -42,7 +49,7 @@ static void keystream_xor(ossl_ctx* x, const uint8_t key[32], const uint8_t nonc
     uint8_t iv[16] = {(uint8_t)ctr, (uint8_t)(ctr >> 8), (uint8_t)(ctr >> 16), (uint8_t)(ctr >> 24), 0, 0, 0, 0};
     memcpy(iv + 8, nonce, 8);
     int len = 0;
-    EVP_EncryptInit_ex(x->c, EVP_chacha20(), NULL, key, iv);
+    EVP_EncryptInit_ex2(x->c, NULL, key, iv, NULL);  /* same cipher, new key / IV */
     EVP_EncryptUpdate(x->c, out, &len, in, (int)n);
 }
 
@@ -98,62 +105,95 @@ int ossl_open(ossl_ctx* x, const uint8_t key[32], const uint8_t nonce[8], const 
     return diff ? 1 : 0;
 }
 
+/* One batch: uniform TLS records (lens == NULL: record i at in + i * stride_in,
+ * n bytes) or a mixed batch (record i at in + in_off[i], lens[i] bytes, key
+ * keys[32 key_index[i]], seq[i]). */
 typedef struct {
-    const uint8_t* key;
+    const uint8_t* keys;
+    const uint32_t* key_index;
+    const uint64_t* seq;
+    const uint32_t* lens;
+    const uint64_t* in_off;
+    const uint64_t* out_off;
     uint64_t seq0;
     const uint8_t* in;
     uint8_t* out;
-    size_t n, begin, end, bad;
+    size_t n, count;
     int open;
+    EVP_CIPHER* cipher;
     EVP_MAC* mac;
+    size_t bad[SP_MAX_THREADS];
 } job;
 
-static void* worker(void* arg) {
+static void task(void* arg, int t, int nt) {
     job* j = (job*)arg;
+    size_t begin, end, bad = 0;
+    sp_range(j->count, t, nt, &begin, &end);
     ossl_ctx x;
-    if (!ossl_init(&x, j->mac)) {
-        j->bad = (size_t)-1;
-        return NULL;
+    if (!ossl_init(&x, j->cipher, j->mac)) {
+        ossl_free(&x);
+        j->bad[t] = (size_t)-1;
+        return;
     }
     uint8_t nonce[8], ad[13];
-    for (size_t i = j->begin; i < j->end; ++i) {
-        tls_nonce_ad(j->seq0 + i, j->n, nonce, ad);
+    for (size_t i = begin; i < end; ++i) {
+        const uint8_t* key = j->lens ? j->keys + 32u * j->key_index[i] : j->keys;
+        const uint64_t seq = j->lens ? j->seq[i] : j->seq0 + i;
+        const size_t len = j->lens ? j->lens[i] : (j->open ? j->n + 16 : j->n);
+        const uint8_t* src = j->lens ? j->in + j->in_off[i] : j->in + i * (j->open ? j->n + 16 : j->n);
+        uint8_t* dst = j->lens ? j->out + j->out_off[i] : j->out + i * (j->open ? j->n : j->n + 16);
+        const size_t n = j->open ? (len >= 16 ? len - 16 : 0) : len;
+        tls_nonce_ad(seq, n, nonce, ad);
         if (!j->open)
-            ossl_seal(&x, j->key, nonce, j->in + i * j->n, j->n, ad, 13, j->out + i * (j->n + 16));
-        else if (ossl_open(&x, j->key, nonce, j->in + i * (j->n + 16), j->n + 16, ad, 13, j->out + i * j->n))
-            j->bad++;
+            ossl_seal(&x, key, nonce, src, n, ad, 13, dst);
+        else if (ossl_open(&x, key, nonce, src, len, ad, 13, dst))
+            bad++;
     }
     ossl_free(&x);
-    return NULL;
+    j->bad[t] = bad;
+}
+
+static size_t run(job* j, int threads) {
+    j->mac = EVP_MAC_fetch(NULL, "POLY1305", NULL);
+    j->cipher = EVP_CIPHER_fetch(NULL, "ChaCha20", NULL);
+    size_t bad = 0;
+    if (!j->mac || !j->cipher) {
+        bad = (size_t)-1;
+    } else {
+        if (threads < 1) threads = 1;
+        if (j->count > 0 && (size_t)threads > j->count) threads = (int)j->count;
+        if (threads > SP_MAX_THREADS) threads = SP_MAX_THREADS;
+        sp_run(task, j, threads);
+        for (int t = 0; t < threads; ++t) {
+            if (j->bad[t] == (size_t)-1) bad = (size_t)-1;
+            else if (bad != (size_t)-1) bad += j->bad[t];
+        }
+    }
+    EVP_MAC_free(j->mac);
+    EVP_CIPHER_free(j->cipher);
+    return bad;
 }
 
 /* TLS-mode batch (same layout and nonce/AD rules as so_*_batch_tls).  Returns
  * the number of records that failed to open (open), or (size_t)-1 when
- * libcrypto cannot provide POLY1305. */
+ * libcrypto cannot provide ChaCha20 / POLY1305. */
 size_t ossl_batch_tls(int open, const uint8_t key[32], uint64_t seq0, const uint8_t* in, size_t n, size_t count,
                       uint8_t* out, int threads) {
-    EVP_MAC* m = EVP_MAC_fetch(NULL, "POLY1305", NULL);
-    if (!m) return (size_t)-1;
-    if (threads < 1) threads = 1;
-    if (count > 0 && (size_t)threads > count) threads = (int)count;
-    job* jobs = (job*)calloc((size_t)threads, sizeof(job));
-    pthread_t* tids = (pthread_t*)calloc((size_t)threads, sizeof(pthread_t));
-    size_t per = (count + (size_t)threads - 1) / (size_t)threads, bad = 0;
-    for (int t = 0; t < threads; ++t) {
-        job* j = &jobs[t];
-        j->key = key; j->seq0 = seq0; j->in = in; j->out = out; j->n = n; j->open = open; j->mac = m;
-        j->begin = (size_t)t * per < count ? (size_t)t * per : count;
-        j->end = j->begin + per < count ? j->begin + per : count;
-        if (threads == 1) worker(j);
-        else pthread_create(&tids[t], NULL, worker, j);
-    }
-    for (int t = 0; t < threads; ++t) {
-        if (threads > 1) pthread_join(tids[t], NULL);
-        if (jobs[t].bad == (size_t)-1) bad = (size_t)-1;
-        else if (bad != (size_t)-1) bad += jobs[t].bad;
-    }
-    free(jobs);
-    free(tids);
-    EVP_MAC_free(m);
+    job* j = (job*)calloc(1, sizeof(job));
+    j->keys = key; j->seq0 = seq0; j->in = in; j->out = out; j->n = n; j->count = count; j->open = open;
+    const size_t bad = run(j, threads);
+    free(j);
+    return bad;
+}
+
+/* Mixed TLS batch (same layout as so_batch_mixed). */
+size_t ossl_batch_mixed(int open, const uint8_t* keys, const uint32_t* key_index, const uint64_t* seq,
+                        const uint32_t* lens, const uint64_t* in_off, const uint64_t* out_off, const uint8_t* in,
+                        uint8_t* out, size_t count, int threads) {
+    job* j = (job*)calloc(1, sizeof(job));
+    j->keys = keys; j->key_index = key_index; j->seq = seq; j->lens = lens; j->in_off = in_off;
+    j->out_off = out_off; j->in = in; j->out = out; j->count = count; j->open = open;
+    const size_t bad = run(j, threads);
+    free(j);
     return bad;
 }

@@ -10,6 +10,7 @@
  * Reference file:line citations are relative to klutzy/suruga.
  */
 #include "suruga_oracle.h"
+#include "so_pool.h"
 
 #include <pthread.h>
 #include <stdlib.h>
@@ -327,20 +328,27 @@ void so_fill_record(uint64_t seed, uint64_t j, uint8_t* buf, size_t n) {
     }
 }
 
+/* The batch drivers below run on the persistent pool of so_pool.h (one
+ * contiguous record range per thread); the reference itself is single-threaded
+ * per connection (cipher/mod.rs:18-23), so threads stand for independent
+ * connections/records. */
 typedef struct {
     const uint8_t* key;
     uint64_t seq0;
     const uint8_t* in;
     uint8_t* out;
     uint8_t* status;
-    size_t n, begin, end, bad;
+    size_t n, count;
+    size_t bad[SP_MAX_THREADS];
     int open;
 } so_job;
 
-static void* so_worker(void* arg) {
+static void so_batch_task(void* arg, int t, int nt) {
     so_job* j = (so_job*)arg;
     uint8_t nonce[8], ad[13];
-    for (size_t i = j->begin; i < j->end; ++i) {
+    size_t begin, end, bad = 0;
+    sp_range(j->count, t, nt, &begin, &end);
+    for (size_t i = begin; i < end; ++i) {
         uint64_t seq = j->seq0 + i;
         so_u64_be(seq, nonce); /* tls.rs:103 */
         so_tls_ad(seq, 23, 3, 3, (uint16_t)j->n, ad);
@@ -350,34 +358,24 @@ static void* so_worker(void* arg) {
             int st = so_open(j->key, nonce, j->in + i * (j->n + 16), j->n + 16, ad, 13,
                              j->out + i * j->n);
             if (j->status) j->status[i] = (uint8_t)st;
-            if (st != SO_OK) j->bad++;
+            if (st != SO_OK) bad++;
         }
     }
-    return NULL;
+    j->bad[t] = bad;
 }
 
 static size_t so_run(const uint8_t key[32], uint64_t seq0, const uint8_t* in, size_t n,
                      size_t count, uint8_t* out, uint8_t* status, int threads, int open) {
     if (threads < 1) threads = 1;
     if (count > 0 && (size_t)threads > count) threads = (int)count;
-    so_job* jobs = (so_job*)calloc((size_t)threads, sizeof(so_job));
-    pthread_t* tids = (pthread_t*)calloc((size_t)threads, sizeof(pthread_t));
-    size_t per = (count + (size_t)threads - 1) / (size_t)threads, bad = 0;
-    for (int t = 0; t < threads; ++t) {
-        so_job* j = &jobs[t];
-        j->key = key; j->seq0 = seq0; j->in = in; j->out = out; j->status = status;
-        j->n = n; j->open = open;
-        j->begin = (size_t)t * per < count ? (size_t)t * per : count;
-        j->end = j->begin + per < count ? j->begin + per : count;
-        if (threads == 1) so_worker(j);
-        else pthread_create(&tids[t], NULL, so_worker, j);
-    }
-    for (int t = 0; t < threads; ++t) {
-        if (threads > 1) pthread_join(tids[t], NULL);
-        bad += jobs[t].bad;
-    }
-    free(jobs);
-    free(tids);
+    if (threads > SP_MAX_THREADS) threads = SP_MAX_THREADS;
+    so_job* j = (so_job*)calloc(1, sizeof(so_job));
+    j->key = key; j->seq0 = seq0; j->in = in; j->out = out; j->status = status;
+    j->n = n; j->count = count; j->open = open;
+    sp_run(so_batch_task, j, threads);
+    size_t bad = 0;
+    for (int t = 0; t < threads; ++t) bad += j->bad[t];
+    free(j);
     return bad;
 }
 
@@ -391,6 +389,63 @@ size_t so_open_batch_tls(const uint8_t key[32], uint64_t seq0, const uint8_t* ct
     return so_run(key, seq0, ct, n, count, pt, status, threads, 1);
 }
 
+/* Mixed TLS batch (C2 shape): record i = in[in_off[i], + lens[i]) (seal: the
+ * plaintext; open: ct || tag, lens[i] >= 16 counting the tag) with key
+ * keys[32 key_index[i]] and sequence number seq[i], output at out + out_off[i].
+ * Returns the number of records whose open status != SO_OK (open only). */
+typedef struct {
+    const uint8_t* keys;
+    const uint32_t* key_index;
+    const uint64_t* seq;
+    const uint32_t* lens;
+    const uint64_t* in_off;
+    const uint64_t* out_off;
+    const uint8_t* in;
+    uint8_t* out;
+    uint8_t* status;
+    size_t count;
+    size_t bad[SP_MAX_THREADS];
+    int open;
+} so_mjob;
+
+static void so_mixed_task(void* arg, int t, int nt) {
+    so_mjob* j = (so_mjob*)arg;
+    uint8_t nonce[8], ad[13];
+    size_t begin, end, bad = 0;
+    sp_range(j->count, t, nt, &begin, &end);
+    for (size_t i = begin; i < end; ++i) {
+        const uint8_t* key = j->keys + 32u * j->key_index[i];
+        const size_t len = j->lens[i];
+        so_u64_be(j->seq[i], nonce);
+        if (!j->open) {
+            so_tls_ad(j->seq[i], 23, 3, 3, (uint16_t)len, ad);
+            so_seal(key, nonce, j->in + j->in_off[i], len, ad, 13, j->out + j->out_off[i]);
+        } else {
+            so_tls_ad(j->seq[i], 23, 3, 3, (uint16_t)(len >= 16 ? len - 16 : 0), ad);
+            int st = so_open(key, nonce, j->in + j->in_off[i], len, ad, 13, j->out + j->out_off[i]);
+            if (j->status) j->status[i] = (uint8_t)st;
+            if (st != SO_OK) bad++;
+        }
+    }
+    j->bad[t] = bad;
+}
+
+size_t so_batch_mixed(int open, const uint8_t* keys, const uint32_t* key_index, const uint64_t* seq,
+                      const uint32_t* lens, const uint64_t* in_off, const uint64_t* out_off, const uint8_t* in,
+                      uint8_t* out, uint8_t* status, size_t count, int threads) {
+    if (threads < 1) threads = 1;
+    if (count > 0 && (size_t)threads > count) threads = (int)count;
+    if (threads > SP_MAX_THREADS) threads = SP_MAX_THREADS;
+    so_mjob* j = (so_mjob*)calloc(1, sizeof(so_mjob));
+    j->keys = keys; j->key_index = key_index; j->seq = seq; j->lens = lens; j->in_off = in_off;
+    j->out_off = out_off; j->in = in; j->out = out; j->status = status; j->count = count; j->open = open;
+    sp_run(so_mixed_task, j, threads);
+    size_t bad = 0;
+    for (int t = 0; t < threads; ++t) bad += j->bad[t];
+    free(j);
+    return bad;
+}
+
 /* XOR-fold of the tags of `count` TLS records sealed with seq = seq0 + i and
  * plaintext record j0 + i of the fill rule (so_fill_record), computed without
  * materialising the batch: the checker of a full-size device run (bench.py
@@ -398,51 +453,42 @@ size_t so_open_batch_tls(const uint8_t key[32], uint64_t seq0, const uint8_t* ct
 typedef struct {
     const uint8_t* key;
     uint64_t seq0, seed, j0;
-    size_t n, begin, end;
-    uint8_t fold[16];
+    size_t n, count;
+    uint8_t fold[SP_MAX_THREADS][16];
 } so_fold_job;
 
-static void* so_fold_worker(void* arg) {
+static void so_fold_task(void* arg, int t, int nt) {
     so_fold_job* j = (so_fold_job*)arg;
     uint8_t* pt = (uint8_t*)malloc(j->n ? j->n : 1);
     uint8_t* ct = (uint8_t*)malloc(j->n + 16);
     uint8_t nonce[8], ad[13];
-    memset(j->fold, 0, 16);
-    for (size_t i = j->begin; i < j->end; ++i) {
+    size_t begin, end;
+    sp_range(j->count, t, nt, &begin, &end);
+    memset(j->fold[t], 0, 16);
+    for (size_t i = begin; i < end; ++i) {
         uint64_t seq = j->seq0 + i;
         so_fill_record(j->seed, j->j0 + i, pt, j->n);
         so_u64_be(seq, nonce);
         so_tls_ad(seq, 23, 3, 3, (uint16_t)j->n, ad);
         so_seal(j->key, nonce, pt, j->n, ad, 13, ct);
-        for (int b = 0; b < 16; ++b) j->fold[b] ^= ct[j->n + b];
+        for (int b = 0; b < 16; ++b) j->fold[t][b] ^= ct[j->n + b];
     }
     free(pt);
     free(ct);
-    return NULL;
 }
 
 void so_tag_fold_tls(const uint8_t key[32], uint64_t seq0, uint64_t seed, uint64_t j0, size_t n, size_t count,
                      int threads, uint8_t out[16]) {
     if (threads < 1) threads = 1;
     if (count > 0 && (size_t)threads > count) threads = (int)count;
-    so_fold_job* jobs = (so_fold_job*)calloc((size_t)threads, sizeof(so_fold_job));
-    pthread_t* tids = (pthread_t*)calloc((size_t)threads, sizeof(pthread_t));
-    size_t per = (count + (size_t)threads - 1) / (size_t)threads;
-    for (int t = 0; t < threads; ++t) {
-        so_fold_job* j = &jobs[t];
-        j->key = key; j->seq0 = seq0; j->seed = seed; j->j0 = j0; j->n = n;
-        j->begin = (size_t)t * per < count ? (size_t)t * per : count;
-        j->end = j->begin + per < count ? j->begin + per : count;
-        if (threads == 1) so_fold_worker(j);
-        else pthread_create(&tids[t], NULL, so_fold_worker, j);
-    }
+    if (threads > SP_MAX_THREADS) threads = SP_MAX_THREADS;
+    so_fold_job* j = (so_fold_job*)calloc(1, sizeof(so_fold_job));
+    j->key = key; j->seq0 = seq0; j->seed = seed; j->j0 = j0; j->n = n; j->count = count;
+    sp_run(so_fold_task, j, threads);
     memset(out, 0, 16);
-    for (int t = 0; t < threads; ++t) {
-        if (threads > 1) pthread_join(tids[t], NULL);
-        for (int b = 0; b < 16; ++b) out[b] ^= jobs[t].fold[b];
-    }
-    free(jobs);
-    free(tids);
+    for (int t = 0; t < threads; ++t)
+        for (int b = 0; b < 16; ++b) out[b] ^= j->fold[t][b];
+    free(j);
 }
 
 /* XOR-fold of the tags of a mixed TLS batch (C2 shape): record i is
@@ -456,46 +502,38 @@ typedef struct {
     const uint32_t* lens;
     const uint64_t* in_off;
     const uint8_t* pt;
-    size_t begin, end;
-    uint8_t fold[16];
+    size_t count;
+    uint8_t fold[SP_MAX_THREADS][16];
 } so_mfold_job;
 
-static void* so_mfold_worker(void* arg) {
+static void so_mfold_task(void* arg, int t, int nt) {
     so_mfold_job* j = (so_mfold_job*)arg;
     uint8_t* ct = (uint8_t*)malloc(65536 + 16);
     uint8_t nonce[8], ad[13];
-    memset(j->fold, 0, 16);
-    for (size_t i = j->begin; i < j->end; ++i) {
+    size_t begin, end;
+    sp_range(j->count, t, nt, &begin, &end);
+    memset(j->fold[t], 0, 16);
+    for (size_t i = begin; i < end; ++i) {
         const size_t n = j->lens[i];
         so_u64_be(j->seq[i], nonce);
         so_tls_ad(j->seq[i], 23, 3, 3, (uint16_t)n, ad);
         so_seal(j->keys + 32u * j->key_index[i], nonce, j->pt + j->in_off[i], n, ad, 13, ct);
-        for (int b = 0; b < 16; ++b) j->fold[b] ^= ct[n + b];
+        for (int b = 0; b < 16; ++b) j->fold[t][b] ^= ct[n + b];
     }
     free(ct);
-    return NULL;
 }
 
 void so_tag_fold_mixed(const uint8_t* keys, const uint32_t* key_index, const uint64_t* seq, const uint32_t* lens,
                        const uint64_t* in_off, const uint8_t* pt, size_t count, int threads, uint8_t out[16]) {
     if (threads < 1) threads = 1;
     if (count > 0 && (size_t)threads > count) threads = (int)count;
-    so_mfold_job* jobs = (so_mfold_job*)calloc((size_t)threads, sizeof(so_mfold_job));
-    pthread_t* tids = (pthread_t*)calloc((size_t)threads, sizeof(pthread_t));
-    size_t per = (count + (size_t)threads - 1) / (size_t)threads;
-    for (int t = 0; t < threads; ++t) {
-        so_mfold_job* j = &jobs[t];
-        j->keys = keys; j->key_index = key_index; j->seq = seq; j->lens = lens; j->in_off = in_off; j->pt = pt;
-        j->begin = (size_t)t * per < count ? (size_t)t * per : count;
-        j->end = j->begin + per < count ? j->begin + per : count;
-        if (threads == 1) so_mfold_worker(j);
-        else pthread_create(&tids[t], NULL, so_mfold_worker, j);
-    }
+    if (threads > SP_MAX_THREADS) threads = SP_MAX_THREADS;
+    so_mfold_job* j = (so_mfold_job*)calloc(1, sizeof(so_mfold_job));
+    j->keys = keys; j->key_index = key_index; j->seq = seq; j->lens = lens; j->in_off = in_off; j->pt = pt;
+    j->count = count;
+    sp_run(so_mfold_task, j, threads);
     memset(out, 0, 16);
-    for (int t = 0; t < threads; ++t) {
-        if (threads > 1) pthread_join(tids[t], NULL);
-        for (int b = 0; b < 16; ++b) out[b] ^= jobs[t].fold[b];
-    }
-    free(jobs);
-    free(tids);
+    for (int t = 0; t < threads; ++t)
+        for (int b = 0; b < 16; ++b) out[b] ^= j->fold[t][b];
+    free(j);
 }

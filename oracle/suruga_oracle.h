@@ -93,6 +93,14 @@ void   so_seal_batch_tls(const uint8_t key[32], uint64_t seq0, const uint8_t* pt
 size_t so_open_batch_tls(const uint8_t key[32], uint64_t seq0, const uint8_t* ct,
                          size_t n, size_t count, uint8_t* pt, uint8_t* status, int threads);
 
+/* Mixed TLS batch (C2 shape, the CPU baseline of bench.py --workload c2):
+ * record i = in[in_off[i], + lens[i]) (open: ct || tag, lens[i] counting the
+ * tag), key keys[32 key_index[i]], sequence number seq[i], output at
+ * out + out_off[i].  Returns the number of failed opens. */
+size_t so_batch_mixed(int open, const uint8_t* keys, const uint32_t* key_index, const uint64_t* seq,
+                      const uint32_t* lens, const uint64_t* in_off, const uint64_t* out_off, const uint8_t* in,
+                      uint8_t* out, uint8_t* status, size_t count, int threads);
+
 /* XOR-fold of the tags of count TLS records (seq = seq0 + i, plaintext =
  * fill-rule record j0 + i) without materialising them. */
 void so_tag_fold_tls(const uint8_t key[32], uint64_t seq0, uint64_t seed, uint64_t j0, size_t n, size_t count,

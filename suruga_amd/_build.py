@@ -28,7 +28,7 @@ HIP_SOURCES = [CSRC / "sg_kernels.hip", CSRC / "sg_wpr.hip", CSRC / "sg_pack.hip
 HIP_DEPS = HIP_SOURCES + [CSRC / "sg_internal.h", CSRC / "sg_device.h", CSRC / "sg_host.h", CSRC / "sg_chacha_grp.inc",
                           ROOT / "include" / "suruga_gpu.h"]
 ORACLE_SOURCES = [ORACLE_DIR / "suruga_oracle.c"]
-ORACLE_DEPS = ORACLE_SOURCES + [ORACLE_DIR / "suruga_oracle.h"]
+ORACLE_DEPS = ORACLE_SOURCES + [ORACLE_DIR / "suruga_oracle.h", ORACLE_DIR / "so_pool.h"]
 
 
 def _stale(target: Path, deps) -> bool:
@@ -36,6 +36,31 @@ def _stale(target: Path, deps) -> bool:
         return True
     t = target.stat().st_mtime
     return any(d.stat().st_mtime > t for d in deps)
+
+
+def source_hash() -> str:
+    """SHA-256 (first 16 hex digits) of every source and header the HIP library
+    is built from (HIP_DEPS, in order, with their names).  The build embeds it
+    (sg_build_info / sg_source_hash), _native.load() refuses a library whose
+    embedded hash differs from the tree's, and build_library() rebuilds on a
+    mismatch whatever the file times say."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for d in HIP_DEPS:
+        h.update(d.name.encode() + b"\0" + d.read_bytes() + b"\0")
+    return h.hexdigest()[:16]
+
+
+def embedded_hash(lib: Path):
+    """The source hash a built library carries (None: none / unreadable)."""
+    import re
+
+    try:
+        m = re.search(rb"sg-src:([0-9a-f]{16})", lib.read_bytes())
+    except OSError:
+        return None
+    return m.group(1).decode() if m else None
 
 
 def _run(cmd) -> None:
@@ -66,13 +91,26 @@ def build_library(force: bool = False, out: Path | None = None, defines=()) -> P
         raise ValueError(f"wrong-output experiment switches are not buildable: {bad}")
     if defines and target.resolve() == LIB.resolve():
         raise ValueError("the product library is built without -D switches; pass out= for a variant")
-    if force or defines or _stale(target, HIP_DEPS):
+    src = source_hash()
+    if force or defines or _stale(target, HIP_DEPS) or embedded_hash(target) != src:
+        import tempfile
+        from concurrent.futures import ThreadPoolExecutor
+
         tmp = target.with_suffix(f".so.tmp{os.getpid()}")  # concurrent builders never share a temp file
         # no wave-aggregating rewrite of atomics: sg_wpr_kernel's group-counter
         # fetch must not wait for its return right away (sg_wpr.hip)
-        _run([hipcc(), "--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17",
-              "-mllvm", "-amdgpu-atomic-optimizer-strategy=None",
-              "-Wall", "-Wno-unused-result", *defines, "-o", str(tmp), *map(str, HIP_SOURCES)])
+        flags = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-mllvm",
+                 "-amdgpu-atomic-optimizer-strategy=None", "-Wall", "-Wno-unused-result", *defines,
+                 f'-DSG_SOURCE_HASH="{src}"']
+        # one translation unit per compiler process (the kernels take most of a
+        # minute each), then one link
+        with tempfile.TemporaryDirectory(prefix="sg_build_") as td:
+            objs = [Path(td) / f"{p.stem}.o" for p in HIP_SOURCES]
+            jobs = int(os.environ.get("MAX_JOBS", "0") or 0) or min(len(HIP_SOURCES), os.cpu_count() or 1)
+            with ThreadPoolExecutor(max_workers=max(1, min(jobs, 16))) as ex:
+                list(ex.map(lambda po: _run([hipcc(), *flags, "-c", "-o", str(po[1]), str(po[0])]),
+                            zip(HIP_SOURCES, objs)))
+            _run([hipcc(), "--offload-arch=gfx950", "-fPIC", "-shared", "-o", str(tmp), *map(str, objs)])
         os.replace(tmp, target)
     return target
 
@@ -116,7 +154,7 @@ def build_ossl(force: bool = False):
     when libcrypto headers are absent."""
     if not Path("/usr/include/openssl/evp.h").exists():
         return OSSL_LIB if OSSL_LIB.exists() else None
-    if force or _stale(OSSL_LIB, [OSSL_SRC]):
+    if force or _stale(OSSL_LIB, [OSSL_SRC, ORACLE_DIR / "so_pool.h"]):
         tmp = OSSL_LIB.with_suffix(f".so.tmp{os.getpid()}")
         _run(["gcc", "-O2", "-std=c11", "-Wall", "-fPIC", "-shared", "-pthread", "-o", str(tmp), str(OSSL_SRC),
               "-lcrypto"])

@@ -20,6 +20,7 @@ SG_E_HIP = -2
 SG_E_NODEV = -3
 
 SG_BATCH_TLS = 0x1
+SG_BATCH_KEEP_FAILED = 0x2
 SG_KEY_LEN = 32
 SG_NONCE_LEN = 8
 SG_MAC_LEN = 16
@@ -32,7 +33,7 @@ EXPORTS = [
     "sg_ctx_new", "sg_ctx_free", "sg_seal", "sg_open",
     "sg_workspace_size", "sg_seal_batch", "sg_open_batch",
     "sg_fill_records", "sg_compare_records",
-    "sg_last_error", "sg_build_info", "sg_set_timing", "sg_timing_read", "sg_set_lockstep", "sg_set_packed",
+    "sg_last_error", "sg_build_info", "sg_source_hash", "sg_set_timing", "sg_timing_read", "sg_set_lockstep", "sg_set_packed",
     "sg_wire_bound", "sg_write_records", "sg_read_records", "sg_record_timing",
     "sg_sha256", "sg_hmac_sha256", "sg_prf_new", "sg_prf_get_bytes", "sg_prf_free",
     "sg_derive_keys", "sg_finished_verify_data",
@@ -125,6 +126,7 @@ def _declare(lib: C.CDLL) -> None:
                                        C.c_uint32, C.c_void_p, C.c_void_p]
     lib.sg_last_error.restype = C.c_char_p
     lib.sg_build_info.restype = C.c_char_p
+    lib.sg_source_hash.restype = C.c_char_p
     lib.sg_set_timing.restype = C.c_int
     lib.sg_set_timing.argtypes = [C.c_int]
     lib.sg_set_lockstep.restype = C.c_int
@@ -176,6 +178,15 @@ def load(path: Path | None = None) -> C.CDLL:
                     "(hipcc --offload-arch=gfx950); there is no CPU fallback")
             lib = C.CDLL(str(p))
             _declare(lib)
+            # provenance: the library must have been built from this tree's
+            # sources (a stale prebuilt .so whose file time happens to be newer
+            # would otherwise run silently)
+            from ._build import source_hash
+
+            got, want = lib.sg_source_hash().decode(), source_hash()
+            if got != want:
+                raise ImportError(f"{p} was built from other sources (embedded hash {got}, tree {want}): "
+                                  "rebuild with `python -m suruga_amd._build`")
             _lib = lib
         return _lib
 

@@ -65,12 +65,13 @@ class Batch:
     ad_stride: int = 0
     status: object = None             # uint8 [count] device (open)
     workspace: object = None          # uint8 [>= workspace_size(count)] device, or None
-    stream: object = None             # torch.cuda.Stream / raw handle / None = current stream
+    stream: object = None             # torch.cuda.Stream / raw handle (0: the NULL stream) / None = current stream
+    keep_failed: bool = False         # open: keep the unauthenticated plaintext of BAD_MAC records
 
     def to_c(self) -> N.SgBatch:
         b = N.SgBatch()
         b.count = self.count
-        b.flags = N.SG_BATCH_TLS if self.tls else 0
+        b.flags = (N.SG_BATCH_TLS if self.tls else 0) | (N.SG_BATCH_KEEP_FAILED if self.keep_failed else 0)
         b.keys = _ptr(self.keys)
         b.num_keys = int(self.keys.shape[0]) if hasattr(self.keys, "shape") and self.keys.dim() == 2 else max(
             1, int(self.keys.numel()) // 32)

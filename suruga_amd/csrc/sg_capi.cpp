@@ -165,7 +165,7 @@ int validate(const sg_batch* b, bool open) {
     if (((uintptr_t)b->keys & 3u) != 0) return fail(SG_E_ARG, "key table must be 4-byte aligned%s");
     if (b->num_keys == 0) return fail(SG_E_ARG, "num_keys must be >= 1%s");
     if (open && !b->status) return fail(SG_E_ARG, "open requires a status array%s");
-    if (b->flags & ~SG_BATCH_TLS) return fail(SG_E_ARG, "unknown flags%s");
+    if (b->flags & ~(SG_BATCH_TLS | SG_BATCH_KEEP_FAILED)) return fail(SG_E_ARG, "unknown flags%s");
     if (!(b->flags & SG_BATCH_TLS)) {
         if (!b->nonces) return fail(SG_E_ARG, "explicit mode needs nonces%s");
         if (b->ad_len > SG_MAX_AD_LEN) return fail(SG_E_ARG, "ad_len exceeds SG_MAX_AD_LEN%s");
@@ -244,20 +244,32 @@ int launch_batch(const sg_batch* b, bool open, hipStream_t s, void* ws) {
         if (timing)
             for (auto& x : e) x = get_event();
     }
-    if (timing) SG_HIP(hipEventRecord(e[0], s));
-    if (wpr) {
-        SG_HIP(sg::launch_wpr(p, open, s, timing ? e[1] : nullptr, timing ? e[2] : nullptr));
-    } else {
-        uint32_t over = 0;
-        SG_HIP(sg::launch_aead(p, open, max_n, uniform, s, &over, timing ? e[1] : nullptr, timing ? e[2] : nullptr));
-        if (over) return fail(SG_E_ARG, "records longer than max_len were not processed%s");
+    // Every launch of the batch is enqueued before any error return: a record
+    // longer than max_len only shows in the population readback, and the
+    // other records' launches (and the timing bookkeeping) still follow it.
+    uint32_t over = 0;
+    hipError_t he = timing ? hipEventRecord(e[0], s) : hipSuccess;
+    if (he == hipSuccess) {
+        if (wpr)
+            he = sg::launch_wpr(p, open, s, timing ? e[1] : nullptr, timing ? e[2] : nullptr);
+        else
+            he = sg::launch_aead(p, open, max_n, uniform, s, &over, timing ? e[1] : nullptr, timing ? e[2] : nullptr);
     }
+    // failed opens hand out no plaintext (chacha20_poly1305.rs:89-93)
+    if (he == hipSuccess && open && !(b->flags & SG_BATCH_KEEP_FAILED)) he = sg::launch_scrub(p, s);
     if (timing) {
-        SG_HIP(hipEventRecord(e[3], s));
+        if (he == hipSuccess) he = hipEventRecord(e[3], s);
         std::lock_guard<std::mutex> lk(g_timing_mu);
-        g_timed.push_back({e[0], e[1], 0});
-        g_timed.push_back({e[2], e[3], open ? 2 : 1});
+        if (he == hipSuccess) {
+            g_timed.push_back({e[0], e[1], 0});
+            g_timed.push_back({e[2], e[3], open ? 2 : 1});
+        } else {
+            for (auto x : e)
+                if (x) g_event_pool.push_back(x);
+        }
     }
+    if (he != hipSuccess) return hip_fail(he, "batch launch");
+    if (over) return fail(SG_E_ARG, "records longer than max_len were not processed%s");
     return SG_OK;
 }
 
@@ -293,9 +305,12 @@ int run_batch(const sg_batch* b, bool open) {
     }
     rc = launch_batch(b, open, s, ws);
     if (cws) ws_release(cws, s, true);
-    if (rc != SG_OK) return rc;
-    if (!b->stream) SG_HIP(hipStreamSynchronize(s));
-    return SG_OK;
+    // NULL stream: the call returns when the batch is done, whatever it returns
+    if (!b->stream) {
+        const hipError_t e = hipStreamSynchronize(s);
+        if (e != hipSuccess && rc == SG_OK) rc = hip_fail(e, "hipStreamSynchronize");
+    }
+    return rc;
 }
 
 }  // namespace
@@ -313,14 +328,22 @@ size_t sg_fixed_iv_len(void) { return 0; }
 size_t sg_mac_len(void) { return SG_MAC_LEN; }
 int sg_abi_version(void) { return SG_ABI_VERSION; }
 const char* sg_last_error(void) { return g_err.c_str(); }
+#ifndef SG_SOURCE_HASH
+#define SG_SOURCE_HASH "0000000000000000"
+#endif
+// the hash of the sources this library was built from (suruga_amd/_build.py
+// source_hash), also findable in the binary as the marker "sg-src:<hash>"
+static const char kSrcMarker[] = "sg-src:" SG_SOURCE_HASH;
+const char* sg_source_hash(void) { return kSrcMarker + 7; }
 const char* sg_build_info(void) {
-    static const std::string pk = std::string("; small records of mixed batches: ") + sg::pack_kernel_config();
+    static const std::string src = std::string(" [") + kSrcMarker + "]";
+    static const std::string pk = std::string("; small records of mixed batches: ") + sg::pack_kernel_config() + src;
     static const std::string on = std::string("gfx950 ") + sg::wpr_kernel_config() + "; other batches: " +
                                   sg::class_kernel_config();
     static const std::string off = std::string("gfx950 ") + sg::class_kernel_config() + " (wave-per-record kernel off)";
-    static const std::string on_pk = on + pk, off_pk = off + pk;
+    static const std::string on_pk = on + pk, off_pk = off + pk, on_s = on + src, off_s = off + src;
     const bool w = sg::wpr_enabled(), k = sg::pack_enabled();
-    return w ? (k ? on_pk.c_str() : on.c_str()) : (k ? off_pk.c_str() : off.c_str());
+    return w ? (k ? on_pk.c_str() : on_s.c_str()) : (k ? off_pk.c_str() : off_s.c_str());
 }
 size_t sg_workspace_size(uint32_t count) {
     // keying records, one list per size class, the class populations and the

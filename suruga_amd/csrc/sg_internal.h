@@ -180,6 +180,8 @@ bool pack_enabled();  // sg_set_packed / SG_PACK environment switch
 int set_pack(int enable);
 hipError_t launch_pack(const KParams& p, bool open, const uint32_t* list, uint32_t count, hipStream_t s);
 const char* pack_kernel_config();
+// zero the output of every record whose open status is 1 (wrong mac)
+hipError_t launch_scrub(const KParams& p, hipStream_t s);
 hipError_t launch_fill(uint8_t* buf, uint64_t stride, uint32_t len, uint32_t count, uint64_t seed,
                        uint64_t j0, hipStream_t s);
 hipError_t launch_compare(const uint8_t* a, uint64_t sa, const uint8_t* b, uint64_t sb, uint32_t len,

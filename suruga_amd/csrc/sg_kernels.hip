@@ -31,6 +31,9 @@
 // All Poly1305 arithmetic is exact mod p = 2^130 - 5, so the tag equals the
 // reference's sequential Horner result bit for bit.
 #include "sg_internal.h"
+
+#include <mutex>
+#include <vector>
 #include "sg_device.h"
 
 #include <stdint.h>
@@ -670,7 +673,33 @@ __global__ __launch_bounds__(256) void sg_compare_kernel(const uint8_t* a, uint6
     }
 }
 
+// Failed opens release no plaintext (chacha20_poly1305.rs:80-93 decrypts
+// unconditionally but returns only Err on a tag mismatch): every record whose
+// status is 1 (wrong mac) gets its output range zeroed after the open
+// kernels, by the wave that finds it.  Records that failed are rare, so the
+// launch costs one status byte per record when none did.  Status 2 (too
+// short) has no output and status 3 (longer than max_len) was never written.
+__global__ __launch_bounds__(256) void sg_scrub_kernel(const KParams p) {
+    const uint32_t base = blockIdx.x * 256u + (threadIdx.x & ~63u), lane = threadIdx.x & 63u;
+    const uint32_t i = base + lane;
+    uint64_t m = __ballot(i < p.count && p.status[i] == 1u);
+    while (m) {
+        const uint32_t rec = base + (uint32_t)__builtin_ctzll(m);
+        m &= m - 1ull;
+        const uint32_t len = record_len(p, rec);
+        const uint32_t n = len >= 16u ? len - 16u : 0u;
+        uint8_t* o = p.out + (p.out_off ? p.out_off[rec] : p.out_stride * rec);
+        for (uint32_t b = lane; b < n; b += 64u) o[b] = 0u;
+    }
+}
+
 }  // namespace
+
+hipError_t launch_scrub(const KParams& p, hipStream_t s) {
+    if (p.count == 0) return hipSuccess;
+    hipLaunchKernelGGL(sg_scrub_kernel, dim3((p.count + 255u) / 256u), dim3(256), 0, s, p);
+    return hipGetLastError();
+}
 
 static hipError_t launch_keying(const KParams& p, bool open, const KeyJobs& jobs, uint32_t grid, hipStream_t s) {
     if (grid == 0) return hipSuccess;
@@ -733,6 +762,33 @@ hipError_t launch_class(uint32_t c, const KParams& q, const uint32_t* list, cons
 #undef SG_CLASS_CASE
 }
 
+// Pinned host buffers for the population readback of mixed batches, shared by
+// every calling thread (a thread_local buffer per caller leaked one pinned
+// allocation per thread that ever ran a mixed batch).  The pool holds at most
+// as many buffers as calls were ever in flight at once; they live as long as
+// the process.
+std::mutex g_pop_mu;
+std::vector<uint32_t*> g_pop_free;
+struct PinnedPop {
+    uint32_t* p = nullptr;
+    hipError_t acquire(size_t bytes) {
+        {
+            std::lock_guard<std::mutex> lk(g_pop_mu);
+            if (!g_pop_free.empty()) {
+                p = g_pop_free.back();
+                g_pop_free.pop_back();
+                return hipSuccess;
+            }
+        }
+        return hipHostMalloc((void**)&p, bytes < 256u ? 256u : bytes, hipHostMallocDefault);
+    }
+    ~PinnedPop() {
+        if (!p) return;
+        std::lock_guard<std::mutex> lk(g_pop_mu);
+        g_pop_free.push_back(p);
+    }
+};
+
 template <bool OPEN>
 hipError_t launch_aead_t(const KParams& p, uint32_t max_n, bool uniform, hipStream_t s, uint32_t* over,
                          hipEvent_t ev_keyed, hipEvent_t ev_start) {
@@ -762,18 +818,18 @@ hipError_t launch_aead_t(const KParams& p, uint32_t max_n, bool uniform, hipStre
     // record is keyed and the classes run on persistent grids instead (and the
     // caller leaves p.wpr_mix off: the wave-per-record buckets need their
     // populations).
-    // (into pinned memory of the calling thread: a DMA, no staging copy)
-    thread_local uint32_t* pop_pinned = nullptr;
+    // (into a pinned buffer from a process-wide pool: a DMA, no staging copy;
+    // the buffer goes back to the pool when this call is done with it)
     uint32_t pop[kNumLists + 1];
     hipStreamCaptureStatus cap_status = hipStreamCaptureStatusNone;
     if ((e = hipStreamIsCapturing(s, &cap_status)) != hipSuccess) return e;
     const bool exact = cap_status == hipStreamCaptureStatusNone;
     if (exact) {
-        if (!pop_pinned && (e = hipHostMalloc((void**)&pop_pinned, sizeof pop, hipHostMallocDefault)) != hipSuccess)
-            return e;
-        if ((e = hipMemcpyAsync(pop_pinned, tail, sizeof pop, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+        PinnedPop pin;
+        if ((e = pin.acquire(sizeof pop)) != hipSuccess) return e;
+        if ((e = hipMemcpyAsync(pin.p, tail, sizeof pop, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
         if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
-        for (uint32_t i = 0; i <= kNumLists; ++i) pop[i] = pop_pinned[i];
+        for (uint32_t i = 0; i <= kNumLists; ++i) pop[i] = pin.p[i];
         *over = pop[kTailOver];
         // size-class keying over the class lists only
         KeyJobs jobs = {};

@@ -14,6 +14,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <deque>
 #include <cstdlib>
 #include <cstring>
 #include <functional>
@@ -38,28 +39,25 @@ double now_ms() {
 }
 }  // namespace
 
-// Host threads for the framing copies of one context (the record bytes move
-// between the caller's buffers and the pinned staging at memcpy speed; one
-// thread alone caps a direction near 9 GB/s).  run(n, fn) calls fn(i) for
-// every i < n on the workers and the calling thread and returns when all are
-// done.  SG_COPY_THREADS sets the total (default 8: tools/record_path_bench.py
+// Host threads for the framing copies (the record bytes move between the
+// caller's buffers and the pinned staging at memcpy speed; one thread alone
+// caps a direction near 9 GB/s).  One pool serves the whole process: it is
+// created on the first call that moves more than one record and its workers
+// then park on a condition variable, so N connections (two contexts each,
+// cipher/mod.rs:18-23) share SG_COPY_THREADS - 1 threads instead of owning
+// 7 each.  run(n, fn) calls fn(i) for every i < n on the workers and the
+// calling thread and returns when all are done; concurrent callers (a
+// reader and a writer thread) each queue a job and the workers take indices
+// from the oldest job that still has some, so both progress.
+// SG_COPY_THREADS sets the total (default 8: tools/record_path_bench.py
 // measured 9.8 / 11.5 / 15.5 / 15.2 GiB/s per direction with 1 / 4 / 8 / 16).
 class CopyPool {
   public:
-    CopyPool() {
-        const char* e = std::getenv("SG_COPY_THREADS");
-        int total = e ? std::atoi(e) : 8;
-        if (total < 1) total = 1;
-        if (total > 32) total = 32;
-        for (int i = 1; i < total; ++i) th_.emplace_back([this] { worker(); });
-    }
-    ~CopyPool() {
-        {
-            std::lock_guard<std::mutex> lk(mu_);
-            stop_ = true;
-        }
-        cv_.notify_all();
-        for (auto& t : th_) t.join();
+    static CopyPool& shared() {
+        // never destroyed: parked workers must not be joined from a static
+        // destructor while the runtime is tearing down
+        static CopyPool* pool = new CopyPool();
+        return *pool;
     }
     void run(uint32_t n, const std::function<void(uint32_t)>& fn) {
         if (n == 0) return;
@@ -67,56 +65,82 @@ class CopyPool {
             for (uint32_t i = 0; i < n; ++i) fn(i);
             return;
         }
+        Job job;
+        job.fn = &fn;
+        job.n = n;
         {
             std::lock_guard<std::mutex> lk(mu_);
-            fn_ = &fn;
-            n_ = n;
-            next_.store(0);
-            busy_ = (uint32_t)th_.size();
-            ++gen_;
+            q_.push_back(&job);
         }
         cv_.notify_all();
-        drain(fn, n);
+        drain(job);
         std::unique_lock<std::mutex> lk(mu_);
-        done_.wait(lk, [this] { return busy_ == 0; });
-        fn_ = nullptr;
+        // no worker can pick the job up once it is off the queue; the ones that
+        // did finish their last index before dropping `active`
+        for (auto it = q_.begin(); it != q_.end(); ++it)
+            if (*it == &job) {
+                q_.erase(it);
+                break;
+            }
+        done_.wait(lk, [&] { return job.active == 0; });
     }
 
   private:
-    void drain(const std::function<void(uint32_t)>& fn, uint32_t n) {
-        for (uint32_t i = next_.fetch_add(1); i < n; i = next_.fetch_add(1)) fn(i);
+    struct Job {
+        const std::function<void(uint32_t)>* fn = nullptr;
+        uint32_t n = 0;
+        std::atomic<uint32_t> next{0};
+        uint32_t active = 0;  // workers inside the job (guarded by mu_)
+    };
+    CopyPool() {
+        const char* e = std::getenv("SG_COPY_THREADS");
+        int total = e ? std::atoi(e) : 8;
+        if (total < 1) total = 1;
+        if (total > 32) total = 32;
+        for (int i = 1; i < total; ++i) th_.emplace_back([this] { worker(); });
+        for (auto& t : th_) t.detach();
+    }
+    static void drain(Job& j) {
+        for (uint32_t i = j.next.fetch_add(1); i < j.n; i = j.next.fetch_add(1)) (*j.fn)(i);
     }
     void worker() {
-        uint64_t seen = 0;
         for (;;) {
-            const std::function<void(uint32_t)>* fn;
-            uint32_t n;
+            Job* j = nullptr;
             {
                 std::unique_lock<std::mutex> lk(mu_);
-                cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
-                if (stop_) return;
-                seen = gen_;
-                fn = fn_;
-                n = n_;
+                for (;;) {
+                    while (!q_.empty() && q_.front()->next.load() >= q_.front()->n) q_.pop_front();  // exhausted
+                    if (!q_.empty()) break;
+                    cv_.wait(lk);
+                }
+                j = q_.front();
+                ++j->active;
             }
-            drain(*fn, n);
-            std::lock_guard<std::mutex> lk(mu_);
-            if (--busy_ == 0) done_.notify_all();
+            drain(*j);
+            {
+                std::lock_guard<std::mutex> lk(mu_);
+                --j->active;
+            }
+            done_.notify_all();
         }
     }
     std::vector<std::thread> th_;
     std::mutex mu_;
     std::condition_variable cv_, done_;
-    const std::function<void(uint32_t)>* fn_ = nullptr;
-    uint32_t n_ = 0;
-    std::atomic<uint32_t> next_{0};
-    uint32_t busy_ = 0;
-    uint64_t gen_ = 0;
-    bool stop_ = false;
+    std::deque<Job*> q_;
 };
 
+// The framing copies of one call: inline for a single record, otherwise on
+// the shared pool (created by the first call that moves more than one).
+void copy_run(uint32_t n, const std::function<void(uint32_t)>& fn) {
+    if (n <= 1) {
+        for (uint32_t i = 0; i < n; ++i) fn(i);
+        return;
+    }
+    CopyPool::shared().run(n, fn);
+}
+
 struct RecordStaging {
-    CopyPool pool;
     struct Slot {
         uint8_t *h_in = nullptr, *h_out = nullptr, *h_meta = nullptr, *h_status = nullptr;
         uint32_t* h_len = nullptr;
@@ -262,7 +286,7 @@ int64_t sg_write_records(sg_ctx* c, uint64_t seq0, uint8_t content_type, uint8_t
     constexpr size_t kWireRec = SG_HEADER_LEN + SG_RECORD_MAX_LEN + SG_MAC_LEN;
     auto emit = [&](RecordStaging::Slot& s) {
         const double t0 = now_ms();
-        rs->pool.run(s.nrec, [&](uint32_t i) {
+        copy_run(s.nrec, [&](uint32_t i) {
             const uint64_t r = s.first + i;
             const uint32_t n = (uint32_t)std::min<uint64_t>(SG_RECORD_MAX_LEN, len - r * SG_RECORD_MAX_LEN);
             uint8_t* h = wire + r * kWireRec;
@@ -289,7 +313,7 @@ int64_t sg_write_records(sg_ctx* c, uint64_t seq0, uint8_t content_type, uint8_t
         if (next < nrec) {
             const uint32_t k = (uint32_t)std::min<uint64_t>(kChunk, nrec - next);
             const double t0 = now_ms();
-            rs->pool.run(k, [&](uint32_t i) {
+            copy_run(k, [&](uint32_t i) {
                 const uint64_t r = next + i;
                 const uint32_t n = (uint32_t)std::min<uint64_t>(SG_RECORD_MAX_LEN, len - r * SG_RECORD_MAX_LEN);
                 std::memcpy(s.h_in + (size_t)i * kSlot, data + r * SG_RECORD_MAX_LEN, n);
@@ -413,7 +437,7 @@ int sg_read_records(sg_ctx* c, uint64_t seq0, const uint8_t* wire, size_t wire_l
             opos += R.flen - SG_MAC_LEN;
             consumed += SG_HEADER_LEN + R.flen;
         }
-        rs->pool.run(ok, [&](uint32_t i) {
+        copy_run(ok, [&](uint32_t i) {
             const uint64_t r = s.first + i;
             const Rec& R = recs[r];
             const uint32_t n = R.flen - SG_MAC_LEN;
@@ -437,7 +461,7 @@ int sg_read_records(sg_ctx* c, uint64_t seq0, const uint8_t* wire, size_t wire_l
             const double t0 = now_ms();
             bool same = true;
             for (uint32_t i = 0; i < k; ++i) same = same && recs[next + i].flen == recs[next].flen;
-            rs->pool.run(k, [&](uint32_t i) {
+            copy_run(k, [&](uint32_t i) {
                 const Rec& R = recs[next + i];
                 const uint64_t seq = seq0 + next + i;
                 std::memcpy(s.h_in + (size_t)i * kSlot, wire + R.off, R.flen);

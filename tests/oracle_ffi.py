@@ -66,6 +66,8 @@ class Oracle:
         L.so_tag_fold_tls.argtypes = [u8p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_size_t, C.c_size_t, C.c_int,
                                       C.c_void_p]
         L.so_tag_fold_mixed.argtypes = [C.c_void_p] * 6 + [C.c_size_t, C.c_int, C.c_void_p]
+        L.so_batch_mixed.restype = C.c_size_t
+        L.so_batch_mixed.argtypes = [C.c_int] + [C.c_void_p] * 9 + [C.c_size_t, C.c_int]
         self.L = L
 
     # --- primitives
@@ -168,6 +170,8 @@ class OsslLine:
         self.L.ossl_batch_tls.restype = C.c_size_t
         self.L.ossl_batch_tls.argtypes = [C.c_int, C.c_char_p, C.c_uint64, C.c_void_p, C.c_size_t, C.c_size_t,
                                           C.c_void_p, C.c_int]
+        self.L.ossl_batch_mixed.restype = C.c_size_t
+        self.L.ossl_batch_mixed.argtypes = [C.c_int] + [C.c_void_p] * 8 + [C.c_size_t, C.c_int]
 
     def seal_batch_tls(self, key, seq0, pt, n, count, threads=1) -> bytes:
         out = C.create_string_buffer((n + 16) * count)

@@ -188,3 +188,44 @@ def test_record_header_parser_without_gpu(lib):
     assert lib.sg_wire_bound(1) == 1 + 21
     assert lib.sg_wire_bound(16384) == 16384 + 21
     assert lib.sg_wire_bound(16385) == 16385 + 42
+
+
+def test_library_carries_the_tree_source_hash(lib):
+    """Provenance: the library embeds the hash of the sources it
+    was built from, and it equals the hash of this tree's sources."""
+    from suruga_amd import _build
+
+    want = _build.source_hash()
+    assert lib.sg_source_hash().decode() == want
+    assert _build.embedded_hash(_build.LIB) == want
+    assert f"sg-src:{want}".encode() in lib.sg_build_info()
+
+
+def test_stale_library_is_refused(tmp_path, lib):
+    """A library built from other sources (here: the product library with its
+    embedded hash rewritten) is refused by the loader, not run."""
+    from suruga_amd import _build
+
+    data = _build.LIB.read_bytes()
+    want = _build.source_hash()
+    other = ("0123456789abcdef" if want != "0123456789abcdef" else "fedcba9876543210").encode()
+    stale = tmp_path / "libsuruga_gpu_stale.so"
+    stale.write_bytes(data.replace(b"sg-src:" + want.encode(), b"sg-src:" + other))
+    code = ("import sys; from pathlib import Path; from suruga_amd import _native as N\n"
+            "try:\n    N.load(Path(sys.argv[1]))\nexcept ImportError as e:\n"
+            "    print('IMPORTERROR', e); raise SystemExit(0)\nraise SystemExit(1)\n")
+    p = subprocess.run([__import__("sys").executable, "-c", code, str(stale)], cwd=ROOT, capture_output=True,
+                       text=True, timeout=120)
+    assert p.returncode == 0 and "IMPORTERROR" in p.stdout and "other sources" in p.stdout, p.stdout + p.stderr
+
+
+def test_unknown_batch_flags_are_rejected(lib):
+    from suruga_amd._native import SG_BATCH_KEEP_FAILED, SG_BATCH_TLS, SG_E_ARG, SgBatch
+
+    b = SgBatch()
+    b.count, b.num_keys = 4, 1
+    b.keys, b.in_, b.out, b.status = 0x1000, 0x2000, 0x3000, 0x4000
+    b.uniform_len, b.in_stride, b.out_stride = 64, 64, 80
+    b.flags = SG_BATCH_TLS | 0x4
+    assert lib.sg_open_batch(C.byref(b)) == SG_E_ARG and b"unknown flags" in lib.sg_last_error()
+    assert SG_BATCH_KEEP_FAILED == 0x2

@@ -65,3 +65,28 @@ def test_bench_two_ranks_one_card(gpu, strong):
     sg = j["scatter_gather"]
     assert sg["verified"] and sg["records_per_rank"] == (2048 if strong else 4096)
     assert sg["scatter_ms"] > 0 and sg["gather_ms"] > 0
+
+
+def test_bench_rejects_gpus_world_size_mismatch():
+    """A launcher's WORLD_SIZE that differs from --gpus is an error, not a
+    silently smaller run (CPU: fails before any GPU call)."""
+    env = dict(os.environ, WORLD_SIZE="3", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2"], capture_output=True, text=True,
+                       timeout=120, env=env, cwd=ROOT)
+    assert p.returncode != 0 and "WORLD_SIZE=3" in (p.stderr + p.stdout)
+
+
+@pytest.mark.gpu
+def test_bench_gpus_two_launches_its_own_ranks(gpu):
+    """`bench.py --gpus 2` with no launcher starts both ranks itself (the form the
+    driver uses), both on the test box's one card with the gloo group."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["SG_DIST_BACKEND"] = "gloo"
+    p = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--records", "4096", "--steps", "2",
+                        "--warmup", "1", "--no-cpu-baseline"], capture_output=True, text=True, timeout=300, cwd=ROOT,
+                       env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    j = _last_json(p.stdout)
+    assert j["n_gpus"] == 2 and j["correct"] and j["scaling"] == "weak"
+    assert j["records_per_s"] * j["ms_per_step"] / 1e3 == pytest.approx(8192, rel=1e-3)
+    assert j["scatter_gather"]["verified"]

@@ -215,7 +215,7 @@ def test_batch_ragged_offsets_keys_and_tamper(gpu, oracle):
     ct_h[int(out_off[5])] ^= 1
     olens = (lens + 16).astype(np.uint32)
     olens[9] = 10
-    back = torch.zeros(pos_i + 16, dtype=torch.uint8, device="cuda")
+    back = torch.full((pos_i + 16,), 0xEE, dtype=torch.uint8, device="cuda")
     st = torch.full((count,), 0xFF, dtype=torch.uint8, device="cuda")
     B.open_(B.Batch(inp=dev_bytes(bytes(ct_h)), out=back, lens=dev(olens), in_off=dev(out_off),
                     out_off=dev(in_off), status=st, **common))
@@ -225,6 +225,8 @@ def test_batch_ragged_offsets_keys_and_tamper(gpu, oracle):
     exp_st[5], exp_st[9] = 1, 2
     assert st_h == bytes(exp_st)
     back_h = host(back)
+    # a record that fails its tag releases no plaintext (chacha20_poly1305.rs:89-93): zero-filled
+    assert back_h[in_off[5]:in_off[5] + lens[5]] == bytes(int(lens[5]))
     for i in range(count):
         if i in (5, 9):
             continue
@@ -615,7 +617,7 @@ def test_mixed_batch_wave_per_record_buckets(gpu, oracle, count):
     st = torch.full((count,), 0xFF, dtype=torch.uint8, device="cuda")
     d_olens = dev(olens)
     B.open_(B.Batch(inp=dev_bytes(bytes(ct_h)), out=back, lens=d_olens, max_len=int(olens.max()), in_off=d_out,
-                    out_off=d_in, status=st, **common))
+                    out_off=d_in, status=st, keep_failed=True, **common))
     torch.cuda.synchronize()
     exp_st = bytearray(count)
     for i in tamper:
@@ -730,7 +732,7 @@ def test_mixed_batch_packed_small_records(gpu, oracle, small_form, count):
     back = torch.zeros(pt_bytes, dtype=torch.uint8, device="cuda")
     st = torch.full((count,), 0xFF, dtype=torch.uint8, device="cuda")
     B.open_(B.Batch(inp=dev_bytes(bytes(ct_h)), out=back, lens=dev(olens), max_len=int(olens.max()),
-                    in_off=dev(out_off), out_off=dev(in_off), status=st, **common))
+                    in_off=dev(out_off), out_off=dev(in_off), status=st, keep_failed=True, **common))
     torch.cuda.synchronize()
     exp_st = bytearray(count)
     for i in tamper:
@@ -746,3 +748,82 @@ def test_mixed_batch_packed_small_records(gpu, oracle, small_form, count):
     i = packed[0]  # decrypted anyway (chacha20_poly1305.rs:80-82)
     o = int(in_off[i])
     assert back_h[o] == pt_h[o] ^ 0x08 and back_h[o + 1:o + int(lens[i])] == pt_h[o + 1:o + int(lens[i])]
+
+
+@pytest.mark.parametrize("keep", [False, True])
+def test_open_failure_output_contract(gpu, oracle, keep):
+    """sg_open_batch on uniform 16 KiB records (the wave-per-record kernel) and on
+    1 KiB records (size classes): a record with a flipped tag byte has status 1
+    and, by default, a zero-filled output (the reference returns only Err,
+    chacha20_poly1305.rs:89-93); with SG_BATCH_KEEP_FAILED its output is the
+    always-computed decryption (:80-82).  The other records are intact."""
+    torch = torch_mod()
+    from suruga_amd import batch as B
+
+    for n, count in ((16384, 24), (1024, 50)):
+        pt = torch.empty(count * n, dtype=torch.uint8, device="cuda")
+        B.fill_records(pt, n, n, count, 0x5EED, j0=0)
+        keys = dev_bytes(KEY).view(1, 32)
+        ct = torch.empty(count * (n + 16), dtype=torch.uint8, device="cuda")
+        B.seal(B.Batch(count=count, keys=keys, inp=pt, out=ct, uniform_len=n, in_stride=n, out_stride=n + 16))
+        bad = (3, count - 1)
+        for i in bad:
+            ct[i * (n + 16) + n + 5] ^= 1
+        back = torch.full((count * n,), 0xEE, dtype=torch.uint8, device="cuda")
+        st = torch.full((count,), 0xFF, dtype=torch.uint8, device="cuda")
+        B.open_(B.Batch(count=count, keys=keys, inp=ct, out=back, uniform_len=n + 16, in_stride=n + 16, out_stride=n,
+                        status=st, keep_failed=keep))
+        torch.cuda.synchronize()
+        exp_st = bytearray(count)
+        for i in bad:
+            exp_st[i] = 1
+        assert host(st) == bytes(exp_st)
+        back_h, pt_h = host(back), host(pt)
+        for i in range(count):
+            got = back_h[i * n:(i + 1) * n]
+            if i in bad:
+                assert got == (pt_h[i * n:(i + 1) * n] if keep else bytes(n)), (n, i)
+            else:
+                assert got == pt_h[i * n:(i + 1) * n], (n, i)
+
+
+def test_overlong_record_on_null_stream(gpu, oracle):
+    """A record longer than max_len on the NULL stream: the call returns SG_E_ARG
+    only after the device work is done, the record's status is 3 (skipped, its
+    output untouched) and every other record is opened correctly."""
+    torch = torch_mod()
+    from suruga_amd import _native as N
+    from suruga_amd import batch as B
+
+    count, n = 40, 512
+    lens = np.full(count, n, dtype=np.uint32)
+    lens[7] = 2000
+    in_off = np.arange(count, dtype=np.uint64) * 4096
+    out_off = np.arange(count, dtype=np.uint64) * 4096
+    pt_h = np.random.default_rng(9).bytes(count * 4096)
+    dev = lambda a: torch.from_numpy(a.view(np.int64) if a.dtype == np.uint64 else a.view(np.int32)).to("cuda")
+    keys = dev_bytes(KEY).view(1, 32)
+    ct = torch.zeros(count * 4096, dtype=torch.uint8, device="cuda")
+    B.seal(B.Batch(count=count, keys=keys, inp=dev_bytes(pt_h), out=ct, lens=dev(lens), max_len=2000,
+                   in_off=dev(in_off), out_off=dev(out_off), seq0=11))
+    torch.cuda.synchronize()
+    back = torch.full((count * 4096,), 0xEE, dtype=torch.uint8, device="cuda")
+    st = torch.full((count,), 0xFF, dtype=torch.uint8, device="cuda")
+    ob = B.Batch(count=count, keys=keys, inp=ct, out=back, lens=dev(lens + 16), max_len=n + 16, in_off=dev(out_off),
+                 out_off=dev(in_off), seq0=11, status=st, stream=0).to_c()
+    import ctypes as C
+
+    rc = N.load().sg_open_batch(C.byref(ob))
+    assert rc == N.SG_E_ARG and "max_len" in N.last_error()
+    # no synchronize here: the NULL-stream call has already finished
+    st_h = bytes(st.cpu().numpy())
+    exp = bytearray(count)
+    exp[7] = 3
+    assert st_h == bytes(exp)
+    back_h = host(back)
+    for i in range(count):
+        o = int(in_off[i])
+        if i == 7:
+            assert back_h[o:o + 2000] == b"\xee" * 2000
+        else:
+            assert back_h[o:o + n] == pt_h[o:o + n], i

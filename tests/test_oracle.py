@@ -206,3 +206,49 @@ def test_tag_fold_mixed_equals_per_record_seals(oracle):
         tag = oracle.seal(k, struct.pack(">Q", s), pt[o:o + n].tobytes(), oracle.tls_ad(s, n))[-16:]
         acc = bytearray(a ^ b for a, b in zip(acc, tag))
     assert fold == bytes(acc)
+
+
+def test_mixed_batch_drivers_match_per_record_seals(oracle):
+    """The C2 CPU baselines (so_batch_mixed, ossl_batch_mixed) seal every record
+    of a Zipf layout exactly as the per-record seal does and open it back;
+    a tampered record fails alone."""
+    import ctypes as C
+    import struct
+
+    import numpy as np
+
+    from oracle_ffi import OsslLine
+    from suruga_amd import workloads as W
+
+    lay = W.c2_layout(200)
+    pt = np.frombuffer(np.random.default_rng(5).bytes(lay.pt_bytes), dtype=np.uint8).copy()
+    seqs = (lay.seq + np.uint64(3)).astype(np.uint64)
+    kb = np.frombuffer(bytes(lay.keys), dtype=np.uint8).copy()
+    ki, lens = lay.key_index.astype(np.uint32), lay.lens.astype(np.uint32)
+    olens = (lens + 16).astype(np.uint32)
+    io, oo = lay.in_off.astype(np.uint64), lay.out_off.astype(np.uint64)
+    P = lambda a: C.c_void_p(a.ctypes.data)  # noqa: E731
+    lines = [("oracle", lambda *a: oracle.L.so_batch_mixed(*a))]
+    try:
+        S = OsslLine().L
+        lines.append(("ossl", lambda op, *a: S.ossl_batch_mixed(op, *a[:8], *a[9:])))
+    except OSError:
+        pass
+    for name, run in lines:
+        ct = np.zeros(lay.ct_bytes, dtype=np.uint8)
+        back = np.zeros(lay.pt_bytes, dtype=np.uint8)
+        st = np.full(lay.count, 9, dtype=np.uint8)
+        assert run(0, P(kb), P(ki), P(seqs), P(lens), P(io), P(oo), P(pt), P(ct), None, lay.count, 3) == 0
+        for i in (0, 1, lay.count // 2, lay.count - 1):
+            k = bytes(lay.keys[32 * int(ki[i]):32 * int(ki[i]) + 32])
+            s, n, a, q = int(seqs[i]), int(lens[i]), int(io[i]), int(oo[i])
+            exp = oracle.seal(k, struct.pack(">Q", s), pt[a:a + n].tobytes(), oracle.tls_ad(s, n))
+            assert ct[q:q + n + 16].tobytes() == exp, name
+        ct[int(oo[7]) + int(lens[7])] ^= 1  # record 7's tag
+        bad = run(1, P(kb), P(ki), P(seqs), P(olens), P(oo), P(io), P(ct), P(back), P(st), lay.count, 3)
+        assert bad == 1, name
+        if name == "oracle":
+            assert st[7] == 1 and int(st.sum()) == 1
+        ok = np.ones(lay.pt_bytes, dtype=bool)
+        ok[int(io[7]):int(io[7]) + int(lens[7])] = False
+        assert np.array_equal(back[ok], pt[ok]), name
