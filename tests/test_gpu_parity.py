@@ -489,8 +489,9 @@ def test_full_record_kernel_geometries(gpu, oracle, kernel_form, adlen):
             mode["ads"] = dev_bytes(bytes(ads_in))
         back = torch.zeros(si * count, dtype=torch.uint8, device="cuda")
         st = torch.full((count,), 0xFF, dtype=torch.uint8, device="cuda")
+        keep = count % 2 == 1  # odd counts: keep the failed records' decryption, even: zero-filled
         B.open_(B.Batch(count=count, keys=keys, inp=dev_bytes(bytes(ct_h)), out=back, uniform_len=n + 16,
-                        in_stride=so, out_stride=si, status=st, **mode))
+                        in_stride=so, out_stride=si, status=st, keep_failed=keep, **mode))
         torch.cuda.synchronize()
         assert host(st) == bytes(exp_st), (kernel_form, adlen, count)
         back_h = host(back)
@@ -498,6 +499,8 @@ def test_full_record_kernel_geometries(gpu, oracle, kernel_form, adlen):
             exp_pt = bytearray(pt_h[i * si:i * si + n])
             if i == 1 and count > 2:
                 exp_pt[4097] ^= 0x01
+            if exp_st[i] and not keep:  # no plaintext with the Err (:89-93)
+                exp_pt = bytearray(n)
             assert back_h[i * si:i * si + n] == bytes(exp_pt), (kernel_form, adlen, count, i)
 
 
