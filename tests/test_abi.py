@@ -5,6 +5,7 @@ No compute calls are made here (there is no GPU in the build container)."""
 from __future__ import annotations
 
 import ctypes as C
+from pathlib import Path
 import re
 import subprocess
 
@@ -229,3 +230,33 @@ def test_unknown_batch_flags_are_rejected(lib):
     b.flags = SG_BATCH_TLS | 0x4
     assert lib.sg_open_batch(C.byref(b)) == SG_E_ARG and b"unknown flags" in lib.sg_last_error()
     assert SG_BATCH_KEEP_FAILED == 0x2
+
+
+def test_no_kernel_uses_scratch(tmp_path, lib):
+    """The wave-per-record and packed kernels count their own vector-memory
+    operations (exact s_waitcnt vmcnt, sg_wpr.hip); a compiler spill to scratch
+    would add vector-memory operations they do not count.  Every kernel of the
+    library must have a zero private segment (no VGPR spills to memory)."""
+    import shutil
+
+    from suruga_amd._build import LIB
+
+    objdump = "/opt/rocm/lib/llvm/bin/llvm-objdump"
+    readelf = "/opt/rocm/lib/llvm/bin/llvm-readelf"
+    if not (Path(objdump).exists() and Path(readelf).exists()):
+        pytest.skip("ROCm llvm tools absent")
+    local = tmp_path / "lib.so"
+    shutil.copy(LIB, local)
+    subprocess.run([objdump, "--offloading", str(local)], cwd=tmp_path, capture_output=True, timeout=120)
+    cos = sorted(tmp_path.glob("lib.so.*gfx950"))
+    assert cos, "no gfx950 code object in the library"
+    seen = 0
+    for co in cos:
+        notes = subprocess.run([readelf, "--notes", str(co)], capture_output=True, text=True, timeout=120).stdout
+        names = re.findall(r"\.name:\s+(\S+)", notes)
+        sizes = [int(x) for x in re.findall(r"\.private_segment_fixed_size:\s+(\d+)", notes)]
+        assert len(names) == len(sizes)
+        for nm, sz in zip(names, sizes):
+            assert sz == 0, f"{nm} uses {sz} bytes of scratch"
+        seen += len(names)
+    assert seen >= 20

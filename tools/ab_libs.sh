@@ -1,16 +1,19 @@
 #!/bin/bash
 # Same-box A/B of library builds: alternating bench runs (C1, 10 steps, no
 # CPU baseline) of every NAME=LIB argument ("-" = the product library), R rounds.
-# Usage (GPU box): R=2 bash tools/ab_libs.sh base=- bar2=tools/exp/lib_bar2.so ...
-set -euo pipefail
+# Variant libraries live in ablib/ (tools/exp/ does not travel to the GPU box).
+# Usage (GPU box): R=2 bash tools/ab_libs.sh base=- v=ablib/lib_v.so ...
+set -uo pipefail
 R=${R:-2}
-OUT=${GRAFT_REPO_ROOT:-.}/gpurun_out/ab_libs
+OUT=${GRAFT_REPO_ROOT:-.}/gpurun_out/ab_libs${AB_TAG:-}
 mkdir -p "$OUT"
 for i in $(seq 1 "$R"); do
   for spec in "$@"; do
     name=${spec%%=*}; lib=${spec#*=}
     if [ "$lib" = "-" ]; then lib=suruga_amd/libsuruga_gpu.so; fi
-    SURUGA_GPU_LIB=$lib timeout -k 10 300 python bench.py --no-cpu-baseline --steps 10 ${BENCH_ARGS:-} > "$OUT/${name}_$i.json" || echo "$name rc=$?"
+    SURUGA_GPU_LIB=$lib timeout -k 10 300 python bench.py --no-cpu-baseline --no-bitexact --steps 10 ${BENCH_ARGS:-} > "$OUT/${name}_$i.json"
+    rc=$?
+    if [ $rc -ne 0 ]; then echo "$name rc=$rc"; exit $rc; fi
     python -c "import json; d=json.loads(open('$OUT/${name}_$i.json').read().strip().splitlines()[-1]); print('$name', '$i', d['value'], 'seal', d['kernel_ms']['seal'], 'open', d['kernel_ms']['open'], 'correct', d['correct'])"
   done
 done
