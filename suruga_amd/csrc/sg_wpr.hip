@@ -432,7 +432,7 @@ __device__ __forceinline__ uint32_t cload(const void* base, uint64_t word) {
 // every DMA of the kernel instead of a 64-bit address per instruction.
 __device__ __forceinline__ void dma_sv(uint32_t l0, const void* sbase, uint32_t voff) {
     uint32_t keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2" SG_DMA_POL "\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep)
                  : "v"(voff), "s"(sbase), "s"(l0)
                  : "memory");
@@ -852,7 +852,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
             // spread over five gaps instead of queueing behind each other.
             auto out_piece = [&](uint32_t k) { return ld16(pb + 1024u * k + 16u * wunit); };
             auto store_piece = [&](uint32_t k, const u32x4& v) {
-                if (!LIST || 1024u * k + 16u * lane >= plo) st16(pend_dst + 1024u * k + 16u * lane, v);
+                if (!LIST || 1024u * k + 16u * lane >= plo) gst16(pend_dst + 1024u * k + 16u * lane, v);
             };
             auto dma_piece = [&](uint32_t k) {
                 const uint32_t ldsb = lds_wave + kWprChunk * (bj ^ 1u);
@@ -1041,7 +1041,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
 #pragma unroll
         for (uint32_t k = 0; k < 4u; ++k)
             if (!LIST || 1024u * k + 16u * lane >= pend_lo)
-                st16(pend_dst + 1024u * k + 16u * lane, ld16(pb + 1024u * k + 16u * wunit));
+                gst16(pend_dst + 1024u * k + 16u * lane, ld16(pb + 1024u * k + 16u * wunit));
     }
 #if SG_WPR_PROFILE
     SG_TICK(t_end);
