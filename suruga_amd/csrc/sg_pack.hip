@@ -69,6 +69,10 @@ __device__ __forceinline__ void pst16(void* p, u32x4 v) {
     if constexpr (SG_PACK_NT_ST) gst16(p, v); else st16(p, v);
 }
 
+#ifndef SG_PACK_IDLE_BARRIERS
+#define SG_PACK_IDLE_BARRIERS 1
+#endif
+
 constexpr uint32_t kPackRecs = 128;                // records per workgroup run
 constexpr uint32_t kPackWaves = 8;                 // two per SIMD: lock-step pairs
 constexpr uint32_t kPackThreads = 64u * kPackWaves;
@@ -296,8 +300,19 @@ __global__ __launch_bounds__(kPackThreads) void sg_pack_kernel(const KParams p, 
     SG_STAMP(7u, 6);
     const uint32_t total = L.total, nchunks = L.nchunks;
     const uint32_t nrounds = (nchunks + kPackWaves - 1u) / kPackWaves;
+    // Chunk order within a round: SIMD pairs first (waves w and w + 4 share a
+    // SIMD), so that in the last, partial round the chunks go to whole pairs
+    // and the waves without one only keep the barrier count (s_barrier, no
+    // VALU): their issue slots go to the CU's other workgroups, and the working
+    // waves stay paired (SG_PACK_IDLE_BARRIERS; round 2 measured that idle waves
+    // running the rounds with EXEC off save only power).
+    const uint32_t pos = 2u * (wave & 3u) + (wave >> 2);
     for (uint32_t k = 0; k < nrounds; ++k) {
-        const uint32_t c = kPackWaves * k + wave;
+        const uint32_t c = kPackWaves * k + (SG_PACK_IDLE_BARRIERS ? pos : wave);
+        if (SG_PACK_IDLE_BARRIERS && c >= nchunks) {  // (wave-uniform) no chunk in this round
+            asm volatile(".rept 80\ns_barrier\n.endr" ::: "memory");  // 10 double rounds x 8 (sg_chacha_grp.inc)
+            continue;
+        }
         const uint32_t b = 64u * c + lane;
         const bool valid = c < nchunks && b < total;
         // the record of run block b: the starts at or before it
@@ -441,9 +456,10 @@ int set_pack(int enable) {
 }
 
 const char* pack_kernel_config() {
-    return "sg_pack_kernel v3: mixed-batch TLS records of 64 B-4 KiB (multiples of 64 B) packed 64-byte block per lane "
+    return "sg_pack_kernel v4: mixed-batch TLS records of 64 B-4 KiB (multiples of 64 B) packed 64-byte block per lane "
            "across 128-record runs (512-thread workgroups, chunk rounds, lock-step grouped ChaCha20 rounds with EXEC limited "
-           "to the lanes holding a block), keying in the same kernel "
+           "to the lanes holding a block; chunks to SIMD pairs first, waves without a chunk in the last round keep "
+           "only the barriers), keying in the same kernel "
            "(block 0, r^(1+32a) and r^(4b) tables in LDS), per-lane Poly1305 share as a 4-step radix-2^32 Horner times "
            "r^(1+4i), LDS atomic accumulation, constant term for AD / length / pads";
 }

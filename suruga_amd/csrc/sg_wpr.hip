@@ -1181,11 +1181,11 @@ int set_wpr(int enable) {
 }
 
 const char* wpr_kernel_config() {
-    return "sg_wpr_kernel v16: full 16 KiB records, one wave per record (8 per 512-thread workgroup, persistent "
+    return "sg_wpr_kernel v17: full 16 KiB records, one wave per record (8 per 512-thread workgroup, persistent "
            "2 per CU, record groups handed out by a device counter), 4 KiB chunks LDS-DMA prefetched lane-contiguously into an XOR-swizzled LDS slice, output "
            "read out during the next chunk's first double rounds, lock-step grouped ChaCha20 rounds (s_barrier per "
            "rotate group; the first double round takes its uniform words from SGPRs, the counter-free steps once "
-           "per record on the SALU), Poly1305 as 16 "
+           "per record on the SALU), non-temporal record stream (nt LDS-DMA loads and stores), Poly1305 as 16 "
            "v_mfma_i32_32x32x32_i8 per record fed from the ciphertext registers one chunk behind (Toeplitz digit "
            "lines of r^(128k+d) in LDS, read as aligned dwords + v_alignbyte), exact per-lane assembly, "
            "W = r^(4(31-q)) scaling, DPP sum; keying pre-pass with the constant term; bucket records: the idle lanes "

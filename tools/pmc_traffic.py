@@ -45,6 +45,28 @@ def main(tag: str, records: int = 1 << 20, record_bytes: int = 16384):
     ks = src / "kt" / "run_kernel_stats.csv"
     if ks.exists():
         shutil.copy(ks, dst / f"{tag}_kernel_stats.csv")
+    # steady state: per kernel, the average duration over its dispatches after
+    # the first SKIP (the first launches run on a GPU coming out of idle), next
+    # to the all-dispatch average of the stats summary
+    kt = src / "kt" / "run_kernel_trace.csv"
+    if kt.exists():
+        per = collections.defaultdict(list)
+        for r in csv.DictReader(open(kt)):
+            per[r["Kernel_Name"]].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+        SKIP = 4
+        rows = []
+        for name, d in per.items():
+            if kind(name) is None and "rocclr" in name:
+                continue
+            steady = d[SKIP:] if len(d) > SKIP else d
+            rows.append({"kernel": name, "dispatches": len(d), "avg_ns_all": round(sum(d) / len(d), 1),
+                         "steady_dispatches": len(steady), "avg_ns_steady": round(sum(steady) / len(steady), 1),
+                         "min_ns": min(d), "max_ns": max(d)})
+        rows.sort(key=lambda x: -x["avg_ns_all"] * x["dispatches"])
+        with open(dst / f"{tag}_kernel_steady.csv", "w", newline="") as fh:
+            w = csv.DictWriter(fh, fieldnames=list(rows[0]) if rows else ["kernel"])
+            w.writeheader()
+            w.writerows(rows)
     # Per BATCH (one sg_seal_batch / sg_open_batch call) sums: a mixed-size batch
     # launches classify + one list kernel per size class; a batch is counted by
     # its keying dispatch.  For C1 a batch is exactly one aead kernel launch.
