@@ -134,6 +134,10 @@ __device__ __forceinline__ uint32_t bytes_from(uint32_t w, uint32_t lo) {
 // accumulator, negated (tests/test_wpr_mac_model.py: CJ)
 constexpr uint32_t kCJ0 = 0x1bd2d2bu, kCJ1 = 0x36f6f6fu, kCJ2 = 0x3dbdbdbu, kCJ3 = 0x2f6f6f6u, kCJ4 = 0x1bdbdbdu;
 
+#ifndef SG_WPR_GEO_TABLES
+#define SG_WPR_GEO_TABLES 1  // bucket keying: geometric sums from the power tables (0: square-and-multiply)
+#endif
+
 // ---------------------------------------------------------------------------
 // Keying pre-pass: one lane per record, 64 records per wave, the 160-word
 // record (sg_internal.h, kW*) staged in LDS by halves and stored coalesced.
@@ -205,21 +209,34 @@ __global__ __launch_bounds__(64) void sg_wpr_keying_kernel(const KParams p, cons
     }
 
     // ---- second half: lo[b] = R^b, hi[h][a] = 2^(32 h) R^(8 a) (R = r^4) ----
+    // (LIST: also the pieces of S(c) = sum_{u<c} R^u, c = (n / 64) & 31, see below)
+    const uint32_t kq = n >> 6, ca = kq >> 5, cl = kq & 7u, ch = (kq >> 3) & 3u;
+    auto sel = [](bool c, const F26& a, const F26& b) {
+        return F26{c ? a.v0 : b.v0, c ? a.v1 : b.v1, c ? a.v2 : b.v2, c ? a.v3 : b.v3, c ? a.v4 : b.v4};
+    };
     const F26 r2 = fmul(r, r), R = fmul(r2, r2);
-    F26 x = f26_one(), sum_lo = f26_zero();
+    F26 x = f26_one(), sum_lo = f26_zero(), plo = f26_zero(), xlo = f26_one();
 #pragma unroll
     for (int b = 0; b < 8; ++b) {
         store_f26(st + (kWLo - 80u) + 5u * b, x);
         sum_lo = f26_add(sum_lo, x);
+        if constexpr (LIST) {
+            plo = sel((uint32_t)b < cl, f26_add(plo, x), plo);  // sum_{b' < c & 7} R^b'
+            xlo = sel((uint32_t)b == cl, x, xlo);               // R^(c & 7)
+        }
         x = fmul(x, R);
     }
     const F26 R8 = x;
-    F26 y = f26_one(), sum_hi = f26_zero();
+    F26 y = f26_one(), sum_hi = f26_zero(), phi = f26_zero(), yc = f26_one();
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
         store_f26(st + (kWHi - 80u) + 5u * a, y);
         store_f26(st + (kWHi - 80u) + 20u + 5u * a, mul_add(y, 0u, 64u, 0u, 0u, 0u, f26_zero()));  // * 2^32
         sum_hi = f26_add(sum_hi, y);
+        if constexpr (LIST) {
+            phi = sel((uint32_t)a < ch, f26_add(phi, y), phi);  // sum_{a' < c >> 3} R^(8 a')
+            yc = sel((uint32_t)a == ch, y, yc);                 // R^(8 (c >> 3))
+        }
         y = fmul(y, R8);
     }
     const F26 T = y;  // R^32 = r^128
@@ -236,22 +253,33 @@ __global__ __launch_bounds__(64) void sg_wpr_keying_kernel(const KParams p, cons
     for (int u = 0; u < 5; ++u) store_f26(st + kWRd + 5u * u, d1 ? pw[u + 1] : pw[u]);
     const F26 rd0 = d1 ? r2 : r;        // r^(1 + delta)
     const F26 rdel = d1 ? r : f26_one();  // r^delta
-    F26 t = f26_one(), sum_t = f26_zero();
+    F26 t = f26_one(), sum_t = f26_zero(), pta = f26_zero(), ta = f26_one();
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
         store_f26(st + kWTk + 5u * k, t);
         sum_t = f26_add(sum_t, t);
+        if constexpr (LIST) pta = sel((uint32_t)k < ca, f26_add(pta, t), pta);  // sum_{k' < a} T^k'
         t = fmul(t, T);
+        if constexpr (LIST) ta = sel((uint32_t)k + 1u == ca, t, ta);            // T^a
     }
 
     // geometric sums: SW = sum_{u<32} R^u; g = G(m) = sum_{i=1..m} r^i and rm = r^m
-    // (m = n / 16: for n = 2^14, G(1024) = (r + r^2 + r^3 + r^4) SW sum_k T^k, r^1024 = T^8)
+    // (m = n / 16: for n = 2^14, G(1024) = (r + r^2 + r^3 + r^4) SW sum_k T^k, r^1024 = T^8).
+    // Bucket records (LIST) have n = 64 k', k' = 32 a + c (a = 2..8, c < 32), so from the
+    // tables: G(4 k') = G4 S(k'), S(k') = sum_{u<k'} R^u = SW sum_{k<a} T^k + T^a S(c),
+    // S(c) = sum_{a'<c>>3} R^(8 a') sum_lo + R^(8 (c>>3)) sum_{b<c&7} R^b, r^m = T^a R^(8 (c>>3)) R^(c&7)
+    // (7 products instead of the ~25 of a square-and-multiply geometric sum)
     const F26 SW = fmul(carry1(sum_hi), carry1(sum_lo));
+    const F26 G4 = carry1(f26_add(f26_add(r, r2), f26_add(r3, R)));
     F26 g, rm;
-    if constexpr (LIST) {
+    if constexpr (LIST && !SG_WPR_GEO_TABLES) {
         g = geo_sum_pow(r, G.m, &rm);
+    } else if constexpr (LIST) {
+        const F26 Sc = fmul_add(yc, carry1(plo), fmul(carry1(phi), carry1(sum_lo)));
+        const F26 Sk = fmul_add(SW, carry1(pta), fmul(ta, Sc));
+        g = fmul(G4, Sk);
+        rm = fmul(ta, fmul(yc, xlo));
     } else {
-        const F26 G4 = carry1(f26_add(f26_add(r, r2), f26_add(r3, R)));
         g = fmul(fmul(G4, SW), carry1(sum_t));
         rm = t;
     }
