@@ -134,6 +134,18 @@ __device__ __forceinline__ uint32_t bytes_from(uint32_t w, uint32_t lo) {
 // accumulator, negated (tests/test_wpr_mac_model.py: CJ)
 constexpr uint32_t kCJ0 = 0x1bd2d2bu, kCJ1 = 0x36f6f6fu, kCJ2 = 0x3dbdbdbu, kCJ3 = 0x2f6f6f6u, kCJ4 = 0x1bdbdbdu;
 
+// keying-table policy experiments: SG_TAB_NT_ST (the keying kernel's stores),
+// SG_TAB_DMA_POL (the record kernel's table DMA)
+#ifndef SG_TAB_NT_ST
+#define SG_TAB_NT_ST 0
+#endif
+#ifndef SG_TAB_DMA_POL
+#define SG_TAB_DMA_POL ""
+#endif
+__device__ __forceinline__ void tab_st16(void* p, u32x4 v) {
+    if constexpr (SG_TAB_NT_ST) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p)); else st16(p, v);
+}
+
 #ifndef SG_WPR_GEO_TABLES
 #define SG_WPR_GEO_TABLES 1  // bucket keying: geometric sums from the power tables (0: square-and-multiply)
 #endif
@@ -152,7 +164,7 @@ __device__ __forceinline__ void wpr_flush_half(const WprList& wl, uint32_t slot0
     for (uint32_t v = lane; v < nvec; v += kWprKeyThreads) {
         const uint32_t rr = v / 20u, c = v - rr * 20u;
         const uint32_t* src = stage + rr * kWprKeyStride + 4u * c;
-        st16(wl.tab + (uint64_t)(slot0 + rr) * kWprRecWords + 80u * half + 4u * c, u32x4{src[0], src[1], src[2], src[3]});
+        tab_st16(wl.tab + (uint64_t)(slot0 + rr) * kWprRecWords + 80u * half + 4u * c, u32x4{src[0], src[1], src[2], src[3]});
     }
 }
 
@@ -468,7 +480,7 @@ __device__ __forceinline__ void dma_sv(uint32_t l0, const void* sbase, uint32_t 
 
 __device__ __forceinline__ void dma_one(uint32_t l0, const void* g) {
     uint32_t keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" SG_TAB_DMA_POL "\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep)
                  : "v"(g), "s"(l0)
                  : "memory");
