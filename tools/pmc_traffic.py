@@ -137,7 +137,10 @@ def main(tag: str, records: int = 1 << 20, record_bytes: int = 16384):
     for line in (log.read_text(errors="replace").splitlines() if log.exists() else []):
         if line.startswith("{") and '"kernels"' in line:
             try:
-                traffic["kernels"] = json.loads(line)["config"]["kernels"]
+                cfgj = json.loads(line)["config"]
+                traffic["kernels"] = cfgj["kernels"]
+                if "layout" in cfgj:
+                    traffic["layout"] = cfgj["layout"]
             except (ValueError, KeyError):
                 pass
     (dst / f"traffic_{tag}.json").write_text(json.dumps(traffic, indent=1) + "\n")
