@@ -53,6 +53,8 @@ def parse():
     # read or written and is not counted in any byte figure.
     ap.add_argument("--c2-ct-align", type=int, default=128,
                     help="C2: alignment of the sealed records (16 = back to back)")
+    ap.add_argument("--c2-pt-align", type=int, default=64,
+                    help="C2: alignment of the plaintext records (64 = back to back)")
     ap.add_argument("--ct-stride", type=int, default=0,
                     help="C1: bytes between sealed records (default: n + 16 rounded up to 128, i.e. 16512; "
                          "n + 16 = back to back)")
@@ -490,7 +492,7 @@ def main():
 
         from suruga_amd import workloads as W
 
-        lay = W.c2_layout(count, ct_align=args.c2_ct_align)
+        lay = W.c2_layout(count, ct_align=args.c2_ct_align, pt_align=args.c2_pt_align)
         t64 = lambda a: torch.from_numpy(a.view(np.int64)).to(dev)
         t32 = lambda a: torch.from_numpy(a.view(np.int32)).to(dev)
         keys = torch.tensor(list(lay.keys), dtype=torch.uint8, device=dev).view(-1, 32)
@@ -498,6 +500,16 @@ def main():
         ct = torch.empty(lay.ct_bytes, dtype=torch.uint8, device=dev)
         back = torch.empty(lay.pt_bytes, dtype=torch.uint8, device=dev)
         B.fill_records(pt, 0, lay.pt_bytes, 1, SEED, j0=seq0)
+        if args.c2_pt_align != 64:  # padding between plaintext records: zero in pt and back (the compare is 64-byte granules)
+            real = torch.zeros(lay.pt_bytes, dtype=torch.bool, device=dev)
+            starts = torch.from_numpy(lay.in_off.view(np.int64)).to(dev)
+            ln = torch.from_numpy(lay.lens.astype(np.int64)).to(dev)
+            mark = torch.zeros(lay.pt_bytes + 1, dtype=torch.int32, device=dev)
+            mark.index_add_(0, starts, torch.ones_like(starts, dtype=torch.int32))
+            mark.index_add_(0, starts + ln, -torch.ones_like(starts, dtype=torch.int32))
+            real = torch.cumsum(mark, 0)[:lay.pt_bytes] > 0
+            pt[~real] = 0
+            back.zero_()
         lens, olens = t32(lay.lens), t32(lay.lens + 16)
         in_off, out_off, kidx = t64(lay.in_off), t64(lay.out_off), t32(lay.key_index)
         seqs = t64(lay.seq + np.uint64(seq0 // 256))
@@ -512,7 +524,9 @@ def main():
         cfg = {"workload": f"C2: {count} TLS records per GPU, Zipf(1.1) sizes 64 B-16 KiB (mean "
                            f"{lay.payload / count:.0f} B), 256 connection keys, seal then open, device-resident",
                            "records_per_gpu": count, "record_bytes": "zipf",
-                           "layout": f"plaintext records back to back; sealed records {args.c2_ct_align}-byte aligned"}
+                           "layout": (f"plaintext records {args.c2_pt_align}-byte aligned"
+                                      + (" (back to back)" if args.c2_pt_align == 64 else "")
+                                      + f"; sealed records {args.c2_ct_align}-byte aligned")}
         cmp_args = (pt, 64, back, 64, 64, lay.pt_bytes // 64)  # 64-byte granules
     seal_c, open_c = seal_b.to_c(), open_b.to_c()
     lib = B.N.load()

@@ -59,19 +59,19 @@ class Layout:
         return int(self.lens.astype(np.uint64).sum())
 
 
-def c2_layout(count: int, num_keys: int = 256, ct_align: int = 16) -> Layout:
-    """ct_align: the sealed records (ct || tag) start on multiples of ct_align
-    bytes (16: back to back, every record 16-byte aligned)."""
+def c2_layout(count: int, num_keys: int = 256, ct_align: int = 16, pt_align: int = 64) -> Layout:
+    """ct_align / pt_align: the sealed records (ct || tag) / plaintext records
+    start on multiples of that many bytes (16 / 64: back to back)."""
     lens = zipf_lengths(count)
     in_off = np.zeros(count, dtype=np.uint64)
     out_off = np.zeros(count, dtype=np.uint64)
     slot = (lens.astype(np.uint64) + 16 + (ct_align - 1)) // ct_align * ct_align
+    pslot = (lens.astype(np.uint64) + (pt_align - 1)) // pt_align * pt_align
     if count > 1:
-        in_off[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+        in_off[1:] = np.cumsum(pslot[:-1], dtype=np.uint64)
         out_off[1:] = np.cumsum(slot[:-1], dtype=np.uint64)
     idx = np.arange(count, dtype=np.uint64)
     key_index = (idx % num_keys).astype(np.uint32)
     seq = (idx // num_keys).astype(np.uint64)
     keys = b"".join(connection_key(j) for j in range(num_keys))
-    pt_bytes = int(lens.astype(np.uint64).sum())
-    return Layout(count, lens, in_off, out_off, key_index, seq, keys, pt_bytes, int(slot.sum()))
+    return Layout(count, lens, in_off, out_off, key_index, seq, keys, int(pslot.sum()), int(slot.sum()))
