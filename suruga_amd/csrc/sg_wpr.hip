@@ -134,18 +134,6 @@ __device__ __forceinline__ uint32_t bytes_from(uint32_t w, uint32_t lo) {
 // accumulator, negated (tests/test_wpr_mac_model.py: CJ)
 constexpr uint32_t kCJ0 = 0x1bd2d2bu, kCJ1 = 0x36f6f6fu, kCJ2 = 0x3dbdbdbu, kCJ3 = 0x2f6f6f6u, kCJ4 = 0x1bdbdbdu;
 
-// keying-table policy experiments: SG_TAB_NT_ST (the keying kernel's stores),
-// SG_TAB_DMA_POL (the record kernel's table DMA)
-#ifndef SG_TAB_NT_ST
-#define SG_TAB_NT_ST 0
-#endif
-#ifndef SG_TAB_DMA_POL
-#define SG_TAB_DMA_POL ""
-#endif
-__device__ __forceinline__ void tab_st16(void* p, u32x4 v) {
-    if constexpr (SG_TAB_NT_ST) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p)); else st16(p, v);
-}
-
 #ifndef SG_WPR_GEO_TABLES
 #define SG_WPR_GEO_TABLES 1  // bucket keying: geometric sums from the power tables (0: square-and-multiply)
 #endif
@@ -157,14 +145,36 @@ __device__ __forceinline__ void tab_st16(void* p, u32x4 v) {
 // bucket), which also writes the slot's descriptor; otherwise slot = record
 // and n = 2^14.
 // ---------------------------------------------------------------------------
+// Table layout in HBM: SG_WPR_TAB_SPLIT (default) stores the two halves of the
+// launch's records as two arrays, half h of slot s at tab + h (count 80) + 80 s,
+// so that a workgroup's flush of one half is one contiguous run of 64 x 320
+// bytes (whole 128-byte lines); SG_WPR_TAB_NT writes them non-temporal, so the
+// table does not sit dirty in the caches while the record kernel streams.
+#ifndef SG_WPR_TAB_SPLIT
+#define SG_WPR_TAB_SPLIT 1
+#endif
+#ifndef SG_WPR_TAB_NT
+#define SG_WPR_TAB_NT 1
+#endif
+__device__ __forceinline__ uint32_t* wpr_tab_half(const WprList& wl, uint32_t slot, uint32_t half) {
+    if constexpr (SG_WPR_TAB_SPLIT) return wl.tab + (uint64_t)half * wl.count * 80u + (uint64_t)slot * 80u;
+    return wl.tab + (uint64_t)slot * kWprRecWords + 80u * half;
+}
 __device__ __forceinline__ void wpr_flush_half(const WprList& wl, uint32_t slot0, uint32_t half, const uint32_t* stage,
                                                uint32_t lane) {
     const uint32_t nrec = wl.count - slot0 < kWprKeyThreads ? wl.count - slot0 : kWprKeyThreads;
     const uint32_t nvec = nrec * 20u;  // 80 words = 20 x 16 B per record and half
+    uint32_t* dst0 = wpr_tab_half(wl, slot0, half);
     for (uint32_t v = lane; v < nvec; v += kWprKeyThreads) {
         const uint32_t rr = v / 20u, c = v - rr * 20u;
         const uint32_t* src = stage + rr * kWprKeyStride + 4u * c;
-        tab_st16(wl.tab + (uint64_t)(slot0 + rr) * kWprRecWords + 80u * half + 4u * c, u32x4{src[0], src[1], src[2], src[3]});
+        const u32x4 val = {src[0], src[1], src[2], src[3]};
+        uint32_t* dst = SG_WPR_TAB_SPLIT ? dst0 + 4u * v : wpr_tab_half(wl, slot0 + rr, half) + 4u * c;
+        if constexpr (SG_WPR_TAB_NT) {
+            __builtin_nontemporal_store(val, reinterpret_cast<u32x4*>(dst));
+        } else {
+            st16(dst, val);
+        }
     }
 }
 
@@ -480,7 +490,7 @@ __device__ __forceinline__ void dma_sv(uint32_t l0, const void* sbase, uint32_t 
 
 __device__ __forceinline__ void dma_one(uint32_t l0, const void* g) {
     uint32_t keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" SG_TAB_DMA_POL "\n\ts_mov_b32 m0, %0"
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep)
                  : "v"(g), "s"(l0)
                  : "memory");
@@ -589,8 +599,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
         // chunk_base: the record's frame chunk start in real addresses (may lie before the record)
         if (!LIST || 1024u * k + 16u * wunit >= lo) dma_sv(uniform(ldsb + 1024u * k), chunk_base + 1024u * k, 16u * wunit);
     };
-    auto dma_table_of = [&](uint32_t slot) {  // into the line area
-        if (lane < kWprRecWords / 4u) dma_one(lds_lines, wl.tab + (uint64_t)slot * kWprRecWords + 4u * lane);
+    auto dma_table_of = [&](uint32_t slot) {  // into the line area (lanes 0-19: half 0, 20-39: half 1)
+        if (lane < kWprRecWords / 4u)
+            dma_one(lds_lines, wpr_tab_half(wl, slot, lane >= 20u ? 1u : 0u) + 4u * (lane >= 20u ? lane - 20u : lane));
     };
     auto dma_desc_of = [&](uint32_t slot) {  // LIST: into the descriptor slot
         if (lane < kWprDescWords / 4u) dma_one(lds_desc, wl.desc + (uint64_t)slot * kWprDescWords + 4u * lane);
