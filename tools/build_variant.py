@@ -1,0 +1,65 @@
+#!/usr/bin/env python3
+"""Build an experiment variant of the HIP library from edited copies of the
+sources into ablib/<name>.so (same-box A/B with tools/ab_libs.sh).
+
+The product sources are never modified: the csrc/ tree is copied to a
+temporary directory, the edits of an edit file are applied there (each edit
+must match exactly once), and the copy is compiled with the product flags and
+the tree's source hash (so that _native.load() accepts the variant when it is
+named by SURUGA_GPU_LIB).  Timing-only variants (skipped work, wrong output)
+live only in ablib/ and in the edit files under tools/variants/.
+
+Usage: python tools/build_variant.py <name> <edits.py> [-DNAME=V ...]
+  edits.py defines EDITS = [(file, old, new), ...]
+"""
+from __future__ import annotations
+
+import runpy
+import shutil
+import subprocess
+import sys
+import tempfile
+from concurrent.futures import ThreadPoolExecutor
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+from suruga_amd import _build  # noqa: E402
+
+
+def main() -> None:
+    name, edit_file, *defines = sys.argv[1:]
+    edits = runpy.run_path(edit_file)["EDITS"] if edit_file != "-" else []
+    out = ROOT / "ablib" / f"{name}.so"
+    out.parent.mkdir(exist_ok=True)
+    with tempfile.TemporaryDirectory(prefix="sg_var_") as td:
+        tdp = Path(td)
+        shutil.copytree(_build.CSRC, tdp / "pkg" / "csrc")  # ../../include resolves as in the tree
+        shutil.copytree(ROOT / "include", tdp / "include")
+        for fname, old, new in edits:
+            f = tdp / "pkg" / "csrc" / fname
+            txt = f.read_text()
+            if txt.count(old) != 1:
+                raise SystemExit(f"edit does not match exactly once in {fname}: {old[:60]!r}")
+            f.write_text(txt.replace(old, new))
+        srcs = [tdp / "pkg" / "csrc" / p.name for p in _build.HIP_SOURCES]
+        flags = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-mllvm",
+                 "-amdgpu-atomic-optimizer-strategy=None", "-Wall", "-Wno-unused-result", f"-I{tdp / 'include'}",
+                 *defines, f'-DSG_SOURCE_HASH="{_build.source_hash()}"']
+        objs = [tdp / f"{s.stem}.o" for s in srcs]
+
+        def cc(so):
+            s, o = so
+            r = subprocess.run([_build.hipcc(), *flags, "-c", "-o", str(o), str(s)], capture_output=True, text=True)
+            if r.returncode:
+                raise SystemExit(r.stderr[-4000:])
+
+        with ThreadPoolExecutor(max_workers=len(srcs)) as ex:
+            list(ex.map(cc, zip(srcs, objs)))
+        subprocess.run([_build.hipcc(), "--offload-arch=gfx950", "-fPIC", "-shared", "-o", str(out),
+                        *map(str, objs)], check=True)
+    print(out)
+
+
+if __name__ == "__main__":
+    main()
