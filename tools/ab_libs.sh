@@ -17,6 +17,6 @@ for i in $(seq 1 "$R"); do
     rc=$?
     # rc 3 = ran but not correct: accepted for timing-only variants (AB_ALLOW_WRONG=1)
     if [ $rc -ne 0 ] && ! { [ $rc -eq 3 ] && [ "${AB_ALLOW_WRONG:-0}" = 1 ]; }; then echo "$name rc=$rc"; exit $rc; fi
-    python -c "import json; d=json.loads(open('$OUT/${name}_$i.json').read().strip().splitlines()[-1]); print('$name', '$i', d['value'], 'seal', d['kernel_ms']['seal'], 'open', d['kernel_ms']['open'], 'correct', d['correct'])"
+    python -c "import json; d=json.loads(open('$OUT/${name}_$i.json').read().strip().splitlines()[-1]); print('$name', '$i', d['value'], 'seal', d['kernel_ms']['seal'], 'open', d['kernel_ms']['open'], 'keying', d['kernel_ms']['keying'], 'correct', d['correct'])"
   done
 done
