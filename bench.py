@@ -394,6 +394,15 @@ def launch_ranks(args):
         sk.bind(("127.0.0.1", 0))
         port = sk.getsockname()[1]
     procs = []
+
+    def forward(signum, _frame):  # a launcher stopped by a signal stops the ranks it started
+        for pr in procs:
+            if pr.poll() is None:
+                pr.send_signal(signal.SIGTERM)
+        raise SystemExit(128 + signum)
+
+    for sig in (signal.SIGTERM, signal.SIGINT, signal.SIGHUP):
+        signal.signal(sig, forward)
     for r in range(args.gpus):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
                    LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
