@@ -106,7 +106,9 @@ typedef struct sg_batch {
     uint32_t flags;            /* SG_BATCH_*                                        */
 
     /* keys: key table [num_keys][32] in device memory; record i uses
-     * key_index[i] (device array) or key 0 when key_index is NULL.            */
+     * key_index[i] (device array) or key 0 when key_index is NULL.  Indices
+     * must be < num_keys; the kernels clamp a larger one to num_keys - 1, so
+     * it never reads outside the table (that record's output is meaningless). */
     const uint8_t*  keys;
     uint32_t        num_keys;
     const uint32_t* key_index;

@@ -198,6 +198,7 @@ int launch_batch(const sg_batch* b, bool open, hipStream_t s, void* ws) {
     std::memset(&p, 0, sizeof p);
     p.keys = b->keys;
     p.key_index = b->key_index;
+    p.num_keys = b->num_keys;
     p.seq = b->seq;
     p.seq0 = b->seq0;
     p.nonces = b->nonces;

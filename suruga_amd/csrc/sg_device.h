@@ -318,7 +318,8 @@ struct RecKey {
 
 __device__ __forceinline__ RecKey record_key(const KParams& p, uint32_t rec) {
     RecKey rk;
-    const uint32_t ki = p.key_index ? p.key_index[rec] : 0u;
+    uint32_t ki = p.key_index ? p.key_index[rec] : 0u;
+    ki = ki < p.num_keys ? ki : p.num_keys - 1u;  // out-of-range indices stay inside the key table
     const uint32_t* kw = reinterpret_cast<const uint32_t*>(p.keys + 32u * ki);
 #pragma unroll
     for (int i = 0; i < 8; ++i) rk.k[i] = kw[i];  // keys are little-endian words (chacha20.rs:37-39)

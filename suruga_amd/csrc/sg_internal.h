@@ -49,6 +49,7 @@ constexpr uint32_t kWprDescWords = 12;
 struct KParams {
     const uint8_t* keys;
     const uint32_t* key_index;
+    uint32_t num_keys;       // >= 1; key indices are clamped to num_keys - 1 (no read outside the table)
     const uint64_t* seq;
     uint64_t seq0;
     const uint8_t* nonces;

@@ -222,7 +222,8 @@ __global__ __launch_bounds__(64) void sg_wpr_keying_kernel(const KParams p, cons
         if constexpr (LIST) {  // the slot's descriptor: where the record lives, its length and nonce
             const uint64_t io = p.in_off ? p.in_off[rec] : p.in_stride * rec;
             const uint64_t oo = p.out_off ? p.out_off[rec] : p.out_stride * rec;
-            const uint32_t ki = p.key_index ? p.key_index[rec] : 0u;
+            uint32_t ki = p.key_index ? p.key_index[rec] : 0u;
+            ki = ki < p.num_keys ? ki : p.num_keys - 1u;  // (record_key's clamp)
             uint32_t* d = wl.desc + (uint64_t)slot * kWprDescWords;
             st16(d, u32x4{(uint32_t)io, (uint32_t)(io >> 32), (uint32_t)oo, (uint32_t)(oo >> 32)});
             st16(d + 4, u32x4{n, rec, ki, rk.n14});
@@ -557,6 +558,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
             d.oo = p.out_stride * slot;
             d.n = kWprN;
             d.ki = p.key_index ? cload(p.key_index, slot) : 0u;
+            d.ki = d.ki < p.num_keys ? d.ki : p.num_keys - 1u;  // (record_key's clamp)
             // nonce (chacha20.rs:25-51; TLS: be64(seq), tls.rs:103)
             if constexpr (TLS) {
                 uint64_t seq = p.seq0 + slot;

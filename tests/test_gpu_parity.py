@@ -830,3 +830,60 @@ def test_overlong_record_on_null_stream(gpu, oracle):
             assert back_h[o:o + 2000] == b"\xee" * 2000
         else:
             assert back_h[o:o + n] == pt_h[o:o + n], i
+
+
+@pytest.mark.parametrize("shape", ["uniform16k", "mixed"])
+def test_key_index_out_of_range_stays_in_table(gpu, oracle, shape):
+    """key_index[i] >= num_keys (a caller bug): the kernels clamp it to
+    num_keys - 1 instead of reading past the key table (suruga_gpu.h), on the
+    wave-per-record path (uniform 16 KiB records) and on every path of a mixed
+    batch; every record is sealed with the key it was given or the clamped one,
+    and opens again."""
+    torch = torch_mod()
+    from suruga_amd import batch as B
+
+    rng = np.random.default_rng(71)
+    count, nk = 600, 4
+    lens = (np.full(count, 16384) if shape == "uniform16k" else
+            np.where(rng.random(count) < 0.5, 64 * rng.integers(1, 257, size=count),
+                     rng.integers(0, 16385, size=count))).astype(np.uint32)
+    step_i = (lens.astype(np.uint64) + 15) // 16 * 16
+    step_o = (lens.astype(np.uint64) + 16 + 15) // 16 * 16
+    in_off = np.zeros(count, dtype=np.uint64)
+    out_off = np.zeros(count, dtype=np.uint64)
+    in_off[1:] = np.cumsum(step_i[:-1])
+    out_off[1:] = np.cumsum(step_o[:-1])
+    pt_bytes, ct_bytes = int(in_off[-1] + step_i[-1]), int(out_off[-1] + step_o[-1])
+    kidx = rng.integers(0, nk, size=count).astype(np.uint32)
+    kidx[::7] = nk
+    kidx[3::11] = 0xFFFFFFFF
+    keys_h = rng.bytes(nk * 32)
+    pt_h = rng.bytes(pt_bytes)
+    dev = lambda a: torch.from_numpy(a.view(np.int64) if a.dtype == np.uint64 else a.view(np.int32)).to("cuda")
+    common = dict(count=count, keys=dev_bytes(keys_h).view(nk, 32), key_index=dev(kidx), seq0=9)
+    ct = torch.zeros(ct_bytes, dtype=torch.uint8, device="cuda")
+    if shape == "uniform16k":
+        B.seal(B.Batch(inp=dev_bytes(pt_h), out=ct, uniform_len=16384, in_stride=16384, out_stride=16400, **common))
+    else:
+        B.seal(B.Batch(inp=dev_bytes(pt_h), out=ct, lens=dev(lens), max_len=int(lens.max()), in_off=dev(in_off),
+                       out_off=dev(out_off), **common))
+    torch.cuda.synchronize()
+    ct_h = host(ct)
+    for i in range(count):
+        k = min(int(kidx[i]), nk - 1)
+        s, n, o, q = 9 + i, int(lens[i]), int(in_off[i]), int(out_off[i])
+        exp = oracle.seal(keys_h[32 * k:32 * k + 32], struct.pack(">Q", s), pt_h[o:o + n], oracle.tls_ad(s, n))
+        assert ct_h[q:q + n + 16] == exp, (i, n, int(kidx[i]))
+    back = torch.zeros(pt_bytes, dtype=torch.uint8, device="cuda")
+    st = torch.full((count,), 0xFF, dtype=torch.uint8, device="cuda")
+    if shape == "uniform16k":
+        B.open_(B.Batch(inp=ct, out=back, uniform_len=16400, in_stride=16400, out_stride=16384, status=st, **common))
+    else:
+        B.open_(B.Batch(inp=ct, out=back, lens=dev((lens + 16).astype(np.uint32)), max_len=int(lens.max()) + 16,
+                        in_off=dev(out_off), out_off=dev(in_off), status=st, **common))
+    torch.cuda.synchronize()
+    assert host(st) == bytes(count)
+    back_h = host(back)
+    for i in range(count):
+        o, n = int(in_off[i]), int(lens[i])
+        assert back_h[o:o + n] == pt_h[o:o + n], (i, n)
