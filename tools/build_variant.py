@@ -10,7 +10,7 @@ named by SURUGA_GPU_LIB).  Timing-only variants (skipped work, wrong output)
 live only in ablib/ and in the edit files under tools/variants/.
 
 Usage: python tools/build_variant.py <name> <edits.py> [-DNAME=V ...]
-  edits.py defines EDITS = [(file, old, new), ...]
+  edits.py defines EDITS = [(file, old, new[, "all"]), ...]
 """
 from __future__ import annotations
 
@@ -36,11 +36,12 @@ def main() -> None:
         tdp = Path(td)
         shutil.copytree(_build.CSRC, tdp / "pkg" / "csrc")  # ../../include resolves as in the tree
         shutil.copytree(ROOT / "include", tdp / "include")
-        for fname, old, new in edits:
+        for fname, old, new, *mode in edits:  # mode "all": every occurrence (at least one)
             f = tdp / "pkg" / "csrc" / fname
             txt = f.read_text()
-            if txt.count(old) != 1:
-                raise SystemExit(f"edit does not match exactly once in {fname}: {old[:60]!r}")
+            n = txt.count(old)
+            if n != 1 and not (mode == ["all"] and n >= 1):
+                raise SystemExit(f"edit matches {n} times in {fname}: {old[:60]!r}")
             f.write_text(txt.replace(old, new))
         srcs = [tdp / "pkg" / "csrc" / p.name for p in _build.HIP_SOURCES]
         flags = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-mllvm",
