@@ -156,6 +156,38 @@ constexpr uint32_t kCJ0 = 0x1bd2d2bu, kCJ1 = 0x36f6f6fu, kCJ2 = 0x3dbdbdbu, kCJ3
 #ifndef SG_WPR_TAB_NT
 #define SG_WPR_TAB_NT 1
 #endif
+// SG_WPR_TAB_GROUPED (default): the records of eight consecutive slots (a
+// record kernel's group) interleaved by 16-byte unit, unit u of slot 8 g + w
+// at tab + 1280 g + 4 (u rows + w) words (rows = 8, or count mod 8 in the last
+// group).  Each lane then stores its own record unit by unit straight from
+// registers and every store instruction still writes whole 128-byte lines (a
+// group's row of one unit), so the keying kernel needs no LDS staging and runs
+// at the occupancy its registers allow; the record kernel's 40 unit reads per
+// record touch lines that the other seven waves of its group read at the same
+// time (the same 640 bytes per record from HBM).
+#ifndef SG_WPR_TAB_GROUPED
+#define SG_WPR_TAB_GROUPED 1
+#endif
+__device__ __forceinline__ uint32_t* wpr_tab_unit(const WprList& wl, uint32_t slot, uint32_t u) {
+    const uint32_t g = slot >> 3, w = slot & 7u;
+    const uint32_t rows = g < (wl.count >> 3) ? 8u : (wl.count & 7u);
+    return wl.tab + (uint64_t)g * (8u * kWprRecWords) + 4u * (u * rows + w);
+}
+// units [U0, U1) of a lane's record (rec: the record's 160 words, registers)
+template <uint32_t U0, uint32_t U1>
+__device__ __forceinline__ void wpr_store_units(const WprList& wl, uint32_t slot, bool act, const uint32_t* rec) {
+    if (!act) return;
+#pragma unroll
+    for (uint32_t u = U0; u < U1; ++u) {
+        const u32x4 val = {rec[4u * u], rec[4u * u + 1u], rec[4u * u + 2u], rec[4u * u + 3u]};
+        u32x4* dst = reinterpret_cast<u32x4*>(wpr_tab_unit(wl, slot, u));
+        if constexpr (SG_WPR_TAB_NT) {
+            __builtin_nontemporal_store(val, dst);
+        } else {
+            st16(dst, val);
+        }
+    }
+}
 __device__ __forceinline__ uint32_t* wpr_tab_half(const WprList& wl, uint32_t slot, uint32_t half) {
     if constexpr (SG_WPR_TAB_SPLIT) return wl.tab + (uint64_t)half * wl.count * 80u + (uint64_t)slot * 80u;
     return wl.tab + (uint64_t)slot * kWprRecWords + 80u * half;
@@ -185,9 +217,15 @@ struct WprKeyJobs {
     uint32_t njobs;
 };
 
+#ifndef SG_WPR_KEY_WAVES
+#define SG_WPR_KEY_WAVES 2  // waves per SIMD the keying kernel is compiled for (4 and more spill to scratch)
+#endif
 template <bool OPEN, bool LIST>
-__global__ __launch_bounds__(64) void sg_wpr_keying_kernel(const KParams p, const WprKeyJobs jobs) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SG_WPR_KEY_WAVES))) void sg_wpr_keying_kernel(
+    const KParams p, const WprKeyJobs jobs) {
+#if !SG_WPR_TAB_GROUPED
     __shared__ uint32_t stage[kWprKeyThreads * kWprKeyStride];
+#endif
     const uint32_t lane = threadIdx.x;
     WprList wl = jobs.b[0];
     uint32_t b0 = 0;
@@ -199,7 +237,14 @@ __global__ __launch_bounds__(64) void sg_wpr_keying_kernel(const KParams p, cons
         }
     const uint32_t slot0 = (blockIdx.x - b0) * kWprKeyThreads;
     const uint32_t slot = slot0 + lane;
+#if SG_WPR_TAB_GROUPED
+    uint32_t rbuf[kWprRecWords];  // the lane's record (registers once unrolled)
+#pragma unroll
+    for (uint32_t i = 0; i < kWprRecWords; ++i) rbuf[i] = 0u;
+    uint32_t* st = rbuf + 80;  // the second half first (offsets below are half-relative)
+#else
     uint32_t* st = stage + lane * kWprKeyStride;
+#endif
     const uint32_t adlen = p.tls ? 13u : p.ad_len;
     if (blockIdx.x == b0 && lane == 0u) *wl.ctr = 0u;  // the record kernel's group counter
 
@@ -263,9 +308,14 @@ __global__ __launch_bounds__(64) void sg_wpr_keying_kernel(const KParams p, cons
         y = fmul(y, R8);
     }
     const F26 T = y;  // R^32 = r^128
+#if SG_WPR_TAB_GROUPED
+    wpr_store_units<20, 40>(wl, slot, act, rbuf);
+    st = rbuf;
+#else
     __syncthreads();
     wpr_flush_half(wl, slot0, 1u, stage, lane);
     __syncthreads();
+#endif
 
     // ---- first half: s, ctot, rd[u] = r^(1 + delta + u), tk[k] = T^k ----
     st[kWS + 0] = s[0]; st[kWS + 1] = s[1]; st[kWS + 2] = s[2]; st[kWS + 3] = s[3];
@@ -285,6 +335,9 @@ __global__ __launch_bounds__(64) void sg_wpr_keying_kernel(const KParams p, cons
         t = fmul(t, T);
         if constexpr (LIST) ta = sel((uint32_t)k + 1u == ca, t, ta);            // T^a
     }
+#if SG_WPR_TAB_GROUPED
+    wpr_store_units<3, 20>(wl, slot, act, rbuf);  // rd and tk now; s and ctot (units 0-2) at the end
+#endif
 
     // geometric sums: SW = sum_{u<32} R^u; g = G(m) = sum_{i=1..m} r^i and rm = r^m
     // (m = n / 16: for n = 2^14, G(1024) = (r + r^2 + r^3 + r^4) SW sum_k T^k, r^1024 = T^8).
@@ -367,8 +420,12 @@ __global__ __launch_bounds__(64) void sg_wpr_keying_kernel(const KParams p, cons
     }
     const F26 ctot = carry1(f26_add(f26_add(f26_add(pads, bias), f26_add(seed, prefix)), suffix));
     store_f26(st + kWCtot, ctot);
+#if SG_WPR_TAB_GROUPED
+    wpr_store_units<0, 3>(wl, slot, act, rbuf);
+#else
     __syncthreads();
     wpr_flush_half(wl, slot0, 0u, stage, lane);
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -601,9 +658,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
         // chunk_base: the record's frame chunk start in real addresses (may lie before the record)
         if (!LIST || 1024u * k + 16u * wunit >= lo) dma_sv(uniform(ldsb + 1024u * k), chunk_base + 1024u * k, 16u * wunit);
     };
-    auto dma_table_of = [&](uint32_t slot) {  // into the line area (lanes 0-19: half 0, 20-39: half 1)
-        if (lane < kWprRecWords / 4u)
-            dma_one(lds_lines, wpr_tab_half(wl, slot, lane >= 20u ? 1u : 0u) + 4u * (lane >= 20u ? lane - 20u : lane));
+    auto dma_table_of = [&](uint32_t slot) {  // into the line area, lane u: unit u
+        if (lane < kWprRecWords / 4u) {
+            if constexpr (SG_WPR_TAB_GROUPED)
+                dma_one(lds_lines, wpr_tab_unit(wl, slot, lane));
+            else
+                dma_one(lds_lines, wpr_tab_half(wl, slot, lane >= 20u ? 1u : 0u) + 4u * (lane >= 20u ? lane - 20u : lane));
+        }
     };
     auto dma_desc_of = [&](uint32_t slot) {  // LIST: into the descriptor slot
         if (lane < kWprDescWords / 4u) dma_one(lds_desc, wl.desc + (uint64_t)slot * kWprDescWords + 4u * lane);
