@@ -447,9 +447,6 @@ def main():
     # rehearsing several ranks on one card (SG_DIST_BACKEND=gloo)
     backend = os.environ.get("SG_DIST_BACKEND", "nccl")
     ndev = torch.cuda.device_count()
-    if backend == "nccl" and world > 1 and ndev and world > ndev:
-        # RCCL needs a GPU per rank (the gloo group may share one, for rehearsals)
-        raise SystemExit(f"bench.py: {world} ranks but {ndev} visible GPUs (SG_DIST_BACKEND=gloo to share one)")
     local_dev = local % ndev if ndev else local
     torch.cuda.set_device(local_dev)
     dev = torch.device("cuda", local_dev)
