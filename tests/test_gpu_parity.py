@@ -354,6 +354,49 @@ def test_mixed_batch_graph_capture(gpu, oracle):
         assert ct_h[q:q + n + 16] == exp, (i, n)
 
 
+def test_full_record_batch_graph_capture(gpu, oracle):
+    """The C1 path (keying pre-pass + wave-per-record kernel) of a seal and an
+    open captured into one HIP graph and replayed twice, the second time on new
+    plaintext and with the sequence numbers moved on (both read from device
+    memory): every record round-trips, and the sealed records equal the
+    oracle's, byte for byte on every tag and on a strided sample."""
+    torch = torch_mod()
+    from suruga_amd import batch as B
+
+    count, n = 2051, 16384
+    keys = dev_bytes(KEY).view(1, 32)
+    pt = torch.empty(count * n, dtype=torch.uint8, device="cuda")
+    ct = torch.zeros(count * (n + 16), dtype=torch.uint8, device="cuda")
+    back = torch.zeros(count * n, dtype=torch.uint8, device="cuda")
+    st = torch.full((count,), 0xFF, dtype=torch.uint8, device="cuda")
+    ws = torch.empty(B.workspace_size(count), dtype=torch.uint8, device="cuda")
+    seq = torch.arange(count, dtype=torch.int64, device="cuda")
+    B.fill_records(pt, n, n, count, SEED, 0)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        cur = torch.cuda.current_stream()
+        B.seal(B.Batch(count=count, keys=keys, inp=pt, out=ct, uniform_len=n, in_stride=n, out_stride=n + 16,
+                       seq=seq, workspace=ws, stream=cur))
+        B.open_(B.Batch(count=count, keys=keys, inp=ct, out=back, uniform_len=n + 16, in_stride=n + 16,
+                        out_stride=n, seq=seq, status=st, workspace=ws, stream=cur))
+    for rnd, (j0, s0) in enumerate([(0, 0), (7 * count, 2**32 - 5)]):
+        B.fill_records(pt, n, n, count, SEED, j0)
+        seq.copy_(torch.arange(count, dtype=torch.int64, device="cuda") + s0)
+        ct.zero_()
+        back.zero_()
+        st.fill_(0xFF)
+        g.replay()
+        torch.cuda.synchronize()
+        assert host(st) == bytes(count) and bool(torch.equal(back, pt)), rnd
+        ref = np.frombuffer(oracle.seal_batch_tls(KEY, s0, host(pt), n, count, threads=min(16, os.cpu_count() or 1)),
+                            dtype=np.uint8).reshape(count, n + 16)
+        got = ct.view(count, n + 16)
+        assert np.array_equal(got[:, n:].cpu().numpy(), ref[:, n:]), rnd
+        for i in list(range(0, count, 257)) + [count - 1]:
+            assert np.array_equal(got[i].cpu().numpy(), ref[i]), (rnd, i)
+
+
 @pytest.mark.parametrize("adlen", [13, 0, 3, 29])
 def test_length_sweep_every_mac_geometry(gpu, oracle, adlen):
     """Every payload length 0..2200 and every 37th length up to 2^14 + 2048 in
