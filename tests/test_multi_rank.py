@@ -1,4 +1,4 @@
-"""Multi-rank path on CPU with gloo, world_size 2: each rank
+"""Multi-rank path on CPU with gloo, world_size 2 and 4: each rank
 seals its own contiguous record range (sequence numbers lo..hi-1, no data-path
 collective), the union over ranks equals the single-process result, and the
 benchmark's timing protocol (barrier + MAX over ranks, suruga_amd.shard.timed)
@@ -68,9 +68,10 @@ def _worker(rank, world, port, expect_fold):
         dist.destroy_process_group()
 
 
-def test_two_ranks_shard_records_gloo(oracle):
+@pytest.mark.parametrize("world", [2, 4])
+def test_ranks_shard_records_gloo(oracle, world):
     expect = _fold(oracle, 0, TOTAL)
-    mp.spawn(_worker, args=(2, _free_port(), expect), nprocs=2, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), expect), nprocs=world, join=True)
 
 
 def test_record_range_partitions():
@@ -126,5 +127,6 @@ def _sg_worker(rank, world, port):
         dist.destroy_process_group()
 
 
-def test_two_ranks_scatter_seal_gather_gloo():
-    mp.spawn(_sg_worker, args=(2, _free_port()), nprocs=2, join=True)
+@pytest.mark.parametrize("world", [2, 4])
+def test_ranks_scatter_seal_gather_gloo(world):
+    mp.spawn(_sg_worker, args=(world, _free_port()), nprocs=world, join=True)
