@@ -29,9 +29,7 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak, /opt/skills/guides/MI355X_MICROARCH.md
-# VALU issue peak: 1024 SIMDs x one wave64 instruction per 2 cycles x 2.4 GHz (same guide);
-# streams mixing ALU kinds issue at ~4 cycles on gfx950 (tools/valu_probe*.hip)
-VALU_PEAK_GIPS = 1024 * 0.5 * 2.4
+SIMDS_PER_CU = 4
 SEED = 0x53555255
 KEY = bytes(range(32))
 METRIC = "GiB/s device-resident ChaCha20-Poly1305 over 16 KiB TLS records, 1/2/4/8 GPUs"
@@ -363,6 +361,89 @@ def measure_scatter_gather(args, dist, backend, rank, world, dev, n, count, seq0
             "note": "root rank 0 -> every rank and back, outside the device-resident value"}
 
 
+def measure_scatter_gather_c2(args, dist, backend, rank, world, dev, lay, keys, stream):
+    """C2 counterpart of measure_scatter_gather: rank 0 holds M = world x
+    --sg-records mixed-size records (the first M of the Zipf layout, each with
+    its connection key and sequence number), splits them into `world`
+    contiguous byte-balanced ranges (shard.byte_balanced_ranges), scatters the
+    plaintext bytes (padded to the largest slice), every rank seals its slice as
+    one mixed batch, and rank 0 gathers the sealed slices and checks each
+    against its own re-seal of the same records.  Every rank derives the
+    slices' metadata from the shared layout; only record bytes travel."""
+    import ctypes as C
+
+    import numpy as np
+    import torch
+
+    from suruga_amd import batch as B
+    from suruga_amd import shard
+
+    M = min(args.sg_records * world, lay.count)
+    lens = lay.lens[:M].astype(np.int64)
+    rng = shard.byte_balanced_ranges(lens, world)
+    in_off = lay.in_off[:M].astype(np.int64)
+    # slice r: plaintext bytes [in_off[lo], end of record hi-1) of the layout; sealed records back to back (16-aligned)
+    pt_span = [(int(in_off[lo]), int(in_off[hi - 1] + lens[hi - 1]) if hi > lo else int(in_off[lo])) for lo, hi in rng]
+    pmax = max(b - a for a, b in pt_span)
+    oslot = (lens + 16 + 15) // 16 * 16
+    ct_len = [int(oslot[lo:hi].sum()) for lo, hi in rng]
+    cmax = max(ct_len)
+    cdev = dev if backend == "nccl" else torch.device("cpu")
+    lib = B.N.load()
+
+    def seal_slice(r, src_dev):
+        lo, hi = rng[r]
+        cnt = hi - lo
+        out = torch.zeros(cmax, dtype=torch.uint8, device=dev)
+        if cnt == 0:
+            return out
+        t64 = lambda a: torch.from_numpy(np.ascontiguousarray(a).astype(np.int64)).to(dev)  # noqa: E731
+        t32 = lambda a: torch.from_numpy(np.ascontiguousarray(a).astype(np.int32)).to(dev)  # noqa: E731
+        ioff = in_off[lo:hi] - in_off[lo]
+        ooff = np.concatenate([[0], np.cumsum(oslot[lo:hi - 1])]).astype(np.int64)
+        ws = torch.empty(B.workspace_size(cnt), dtype=torch.uint8, device=dev)
+        b = B.Batch(count=cnt, keys=keys, inp=src_dev, out=out, lens=t32(lens[lo:hi]), max_len=int(lens[lo:hi].max()),
+                    in_off=t64(ioff), out_off=t64(ooff), key_index=t32(lay.key_index[lo:hi]),
+                    seq=t64(lay.seq[lo:hi].astype(np.int64)), workspace=ws, stream=stream).to_c()
+        B.N.check(lib.sg_seal_batch(C.byref(b)))
+        torch.cuda.synchronize()
+        return out
+
+    src_chunks = gather_chunks = None
+    if rank == 0:
+        full = torch.empty(pt_span[-1][1], dtype=torch.uint8, device=dev)
+        B.fill_records(full, 0, full.numel(), 1, SEED, j0=0)
+        src_chunks, gather_chunks = [], []
+        for a, b_ in pt_span:
+            t = torch.zeros(pmax, dtype=torch.uint8, device=dev)
+            t[:b_ - a] = full[a:b_]
+            src_chunks.append(t.to(cdev))
+            gather_chunks.append(torch.empty(cmax, dtype=torch.uint8, device=cdev))
+    mine = torch.empty(pmax, dtype=torch.uint8, device=cdev)
+    sync = torch.cuda.synchronize
+    dd = dev if backend == "nccl" else None
+    scatter_s = shard.timed_collective(dist, lambda: shard.scatter_records(dist, 0, mine, src_chunks), sync=sync,
+                                       device=dd)
+    sealed = seal_slice(rank, mine.to(dev))
+    sealed_c = sealed.to(cdev)
+    gather_s = shard.timed_collective(dist, lambda: shard.gather_records(dist, 0, sealed_c, gather_chunks),
+                                      sync=sync, device=dd)
+    ok = True
+    if rank == 0:
+        for r in range(world):
+            ok = ok and bool(torch.equal(seal_slice(r, src_chunks[r].to(dev))[:ct_len[r]],
+                                         gather_chunks[r].to(dev)[:ct_len[r]]))
+    ok_all = sum_over_ranks(dist, 0.0 if ok else 1.0, dd) == 0.0
+    moved_in = sum(b - a for a, b in pt_span[1:])
+    moved_out = sum(ct_len[1:])
+    return {"records": M, "split": "byte_balanced_ranges", "ranges": [list(x) for x in rng],
+            "backend": "rccl" if backend == "nccl" else backend,
+            "scatter_ms": round(scatter_s * 1e3, 3), "gather_ms": round(gather_s * 1e3, 3),
+            "scatter_GBps": round(moved_in / scatter_s / 1e9, 2), "gather_GBps": round(moved_out / gather_s / 1e9, 2),
+            "verified": ok_all,
+            "note": "root rank 0 -> every rank and back (slices padded to the largest), outside the device-resident value"}
+
+
 def sum_over_ranks(dist, value, device=None):
     if dist is None:
         return value
@@ -371,6 +452,95 @@ def sum_over_ranks(dist, value, device=None):
     t = torch.tensor([float(value)], dtype=torch.float64, device=device)
     dist.all_reduce(t)
     return float(t.item())
+
+
+def issue_roofline(dom, workload, count, cus, dom_ms, tj, isa, sclk_mhz):
+    """The dominant launch against its VALU issue bound at the clock it ran at
+    (VERDICT r3 item 2).  Model (profiles/r01_valu_issue_probes.md): a wave64
+    VALU instruction costs 2 SIMD clocks when it is a v_add / v_xor of the
+    lock-step ARX asm (paired with its SIMD partner wave), 4 otherwise
+    (rotates, every non-ARX instruction).  Instruction counts: the PMC
+    SQ_INSTS_VALU of this build's profile (tj, per launch) split by the static
+    census of the same sources (isa: tools/isa_census.py).  bound_ms = issue
+    clocks per SIMD / sclk; frac = bound_ms / measured launch time (<= 1 when
+    the model holds: the rest is stalls, barriers and launch tails)."""
+    if not isa or not sclk_mhz:
+        return {"bound": "valu", "unavailable": "no ISA census of this build" if not isa else "no sclk reading"}
+    kern = isa["kernels"]
+    simds = cus * SIMDS_PER_CU
+    op = "true" if dom == "open" else "false"
+    if workload == "c1":
+        name = f"void sg::(anonymous namespace)::sg_wpr_kernel<{op}, true, 4u, false>(sg::KParams, sg::WprList)"
+        k = kern.get(name)
+        if k is None:
+            return {"bound": "valu", "unavailable": f"{name} not in the census"}
+        vpr = (tj or {}).get(f"{dom}_valu_per_record")
+        src = "PMC SQ_INSTS_VALU per record (profile of this build)" if vpr else "static census (no PMC profile)"
+        vpr = vpr or k["valu"]
+        arx = k["arx_full"] + k["arx_rot"]
+        clk_rec = 2 * k["arx_full"] + 4 * k["arx_rot"] + 4 * max(vpr - arx, 0.0)
+        clk = clk_rec * count / simds
+        per = {"valu_per_record": round(vpr, 1), "arx_full_per_record": k["arx_full"],
+               "arx_rot_per_record": k["arx_rot"], "other_valu_per_record": round(max(vpr - arx, 0.0), 1),
+               "issue_clk_per_record": round(clk_rec, 1), "valu_source": src}
+    else:
+        byk = (tj or {}).get(f"{dom}_valu_by_kernel")
+        if not byk:
+            return {"bound": "valu", "unavailable": "no per-kernel PMC VALU counts of this build"}
+        clk, per, miss = 0.0, {}, []
+        for name, v in byk.items():
+            k = kern.get(name)
+            if k is None or not k.get("clk_per_valu"):
+                miss.append(name)
+                continue
+            clk += v * k["clk_per_valu"] / simds
+            per[name] = {"valu": round(v), "clk_per_valu": k["clk_per_valu"]}
+        per = {"kernels": per, "not_in_census": miss,
+               "valu_source": "PMC SQ_INSTS_VALU per kernel and batch, priced with each kernel's static mix"}
+    bound_ms = clk / (sclk_mhz * 1e3)
+    return dict({"bound": "valu", "model": isa.get("model"), "sclk_mhz": sclk_mhz, "simds": simds,
+                 "issue_bound_ms": round(bound_ms, 4), "avg_launch_ms": round(dom_ms, 4),
+                 "frac": round(bound_ms / dom_ms, 4)}, **per)
+
+
+def gather_over_ranks(dist, obj):
+    """Every rank's `obj`, in rank order, on every rank (one entry without a group)."""
+    if dist is None:
+        return [obj]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, obj)
+    return out
+
+
+def rank_verdict(dist, mine: dict):
+    """AND of every rank's correctness flags (rank 0 used to print
+    its own).  `mine`: this rank's {"rank", "local_rank", "device",
+    "roundtrip_ok", "bitexact_fold", "bitexact_sample"} (None = not checked).
+    Returns (correct over all ranks, the per-rank list, the AND of each
+    bit-exactness flag over the ranks that checked it)."""
+    ranks = gather_over_ranks(dist, mine)
+    correct = all(r["roundtrip_ok"] and r.get("bitexact_fold") is not False and r.get("bitexact_sample") is not False
+                  for r in ranks)
+    flags = {}
+    for k in ("bitexact_fold", "bitexact_sample"):
+        vals = [r.get(k) for r in ranks if r.get(k) is not None]
+        flags[k] = all(vals) if vals else None
+    return correct, ranks, flags
+
+
+def correctness_fields(correct, ranks, flags, exact):
+    """The line's correctness keys: rank 0's check details, overridden by the
+    AND over every rank (a failing rank turns "correct" and its flag false)."""
+    out = dict(exact or {})
+    out.update({k: v for k, v in flags.items() if v is not None})
+    out["correct"] = correct
+    out["ranks"] = ranks
+    return out
+
+
+def exit_code(correct: bool) -> int:
+    """Every rank exits 3 when any rank's check failed (0 otherwise)."""
+    return 0 if correct else 3
 
 
 def launch_ranks(args):
@@ -548,8 +718,16 @@ def main():
     torch.cuda.synchronize()  # inputs and tables made on the default stream
     for _ in range(args.warmup):
         step()
+    # the shader clock and board power over the timed region (sysfs, plain reads
+    # on a background thread): the issue-bound roofline is priced at this clock
+    from suruga_amd import devmon
+
+    props = torch.cuda.get_device_properties(dev)
+    bus = f"{props.pci_domain_id:04x}:{props.pci_bus_id:02x}:{props.pci_device_id:02x}.0"
+    sampler = devmon.Sampler(bus).start()
     elapsed = shard.timed(dist, step, args.steps, sync=torch.cuda.synchronize,
                           device=dev if backend == "nccl" else None)
+    mon = sampler.stop()
 
     # per-kernel device time with HIP events on the launch stream, right after
     # the timed steps while the GPU is still at its steady-state clock (round 2
@@ -561,7 +739,8 @@ def main():
     B.set_timing(False)
 
     # correctness of the last step (outside the timed region): every record
-    # round-trips, and (C1) every tag and a sample of records equal the oracle's
+    # round-trips, and every tag and a sample of records equal the oracle's;
+    # the verdict is the AND over all ranks
     mism = torch.zeros(1, dtype=torch.int64, device=dev)
     B.compare_records(*cmp_args, mism, stream=stream)
     torch.cuda.synchronize()
@@ -572,13 +751,21 @@ def main():
         torch.cuda.synchronize()
         exact = bitexact_check(ct, n, count, seq0, cs) if args.workload == "c1" else \
             bitexact_check_c2(lay, pt, ct, seq0 // 256)
-        roundtrip_ok = roundtrip_ok and exact["bitexact_fold"] and exact["bitexact_sample"]
+    if os.environ.get("SG_BENCH_CORRUPT_RANK") == str(rank) and exact is not None:
+        exact["bitexact_fold"] = False  # test hook (tests/test_bench_contract.py): a rank whose check fails
+    mine = {"rank": rank, "local_rank": local, "device": local_dev, "pci_bus": bus, "roundtrip_ok": roundtrip_ok,
+            "bitexact_fold": exact["bitexact_fold"] if exact else None,
+            "bitexact_sample": exact["bitexact_sample"] if exact else None}
+    correct, ranks, flags = rank_verdict(dist, mine)
 
     scatter_gather = None
-    if world > 1 and args.sg_records > 0 and args.workload == "c1":
+    if world > 1 and args.sg_records > 0:
         try:  # a side measurement: a failure here is reported, not fatal to the device-resident line
-            scatter_gather = measure_scatter_gather(args, dist, backend, rank, world, dev, n, count, seq0, seal_b,
-                                                    lib, keys, ws, stream)
+            if args.workload == "c1":
+                scatter_gather = measure_scatter_gather(args, dist, backend, rank, world, dev, n, count, seq0, seal_b,
+                                                        lib, keys, ws, stream)
+            else:
+                scatter_gather = measure_scatter_gather_c2(args, dist, backend, rank, world, dev, lay, keys, stream)
         except (RuntimeError, ValueError) as e:
             scatter_gather = {"error": f"{type(e).__name__}: {e}"[:300]}
 
@@ -598,13 +785,12 @@ def main():
     achieved_read = alg_read[dom] / (dom_ms * 1e-3) / 1e9
     # the event-timed kernels of one step against the wall-clock step
     kernel_sum_ms = tm["seal_ms"] + tm["open_ms"] + 2 * tm["keying_ms"]
-    traffic, valu, traffic_src = None, None, None
+    traffic, traffic_src, tj = None, None, None
     # the PMC traffic summary of this exact kernel build and workload (the newest
     # profiles/traffic_*.json whose build string and record shape match)
     build = lib.sg_build_info().decode()
     cands = [Path(args.traffic)] if args.traffic else sorted(
         (ROOT / "profiles").glob("traffic_*.json"), key=lambda q: q.stat().st_mtime, reverse=True)
-    tp = None
     for q in cands:
         try:
             tq = json.loads(q.read_text())
@@ -613,27 +799,22 @@ def main():
         if tq.get("records") == count and tq.get("record_bytes") == cfg["record_bytes"] and \
                 tq.get("kernels") == build and tq.get("layout") == cfg.get("layout") and \
                 tq.get(f"{dom}_bytes_per_launch"):
-            tp = q
+            tj = tq
+            traffic = tq.get(f"{dom}_bytes_per_launch")
+            traffic_src = (f"profiles/{q.name}: rocprofv3 PMC FETCH_SIZE x 2 + WRITE_SIZE of this kernel build "
+                           "and record layout in a separate profiling run (not this run)")
             break
-    if tp is not None:
+    # the static ISA census of the loaded library's sources (tools/isa_census.py)
+    provenance = B.N.loaded_info()
+    isa = None
+    isa_path = ROOT / "profiles" / f"isa_{provenance['source_hash']}.json"
+    if isa_path.exists():
         try:
-            tj = json.loads(tp.read_text())
-            if True:
-                traffic = tj.get(f"{dom}_bytes_per_launch")
-                traffic_src = (f"profiles/{tp.name}: rocprofv3 PMC FETCH_SIZE x 2 + WRITE_SIZE of this kernel build "
-                               "and record layout in a separate profiling run (not this run)") if traffic else None
-                vpr = tj.get(f"{dom}_valu_per_record")
-                if vpr:
-                    # VALU issue account of the same kernel: PMC SQ_INSTS_VALU per record (a
-                    # property of the code, from the profile) / this run's launch time
-                    ips = vpr * count / (dom_ms * 1e-3)
-                    valu = {"bound": "valu", "instr_per_record": round(vpr, 1),
-                            "achieved": round(ips / 1e9, 1), "unit": "G wave-instr/s",
-                            "peak": VALU_PEAK_GIPS, "frac": round(ips / 1e9 / VALU_PEAK_GIPS, 4),
-                            "peak_mixed_stream": VALU_PEAK_GIPS / 2,
-                            "frac_mixed_stream": round(ips / 1e9 / (VALU_PEAK_GIPS / 2), 4)}
-        except (ValueError, OSError):
-            traffic = None
+            isa = json.loads(isa_path.read_text())
+        except ValueError:
+            isa = None
+    sclk = (mon.get("sclk_mhz") or {}).get("mean")
+    valu = issue_roofline(dom, args.workload, count, props.multi_processor_count, dom_ms, tj, isa, sclk)
 
     wpr_on = args.workload == "c1" and n == 16384 and lib.sg_set_lockstep(-1) == 1
     if args.workload == "c1":
@@ -650,7 +831,8 @@ def main():
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True, "scaling": "strong" if args.strong else "weak", "vs_baseline": None, "dtype": "u32",
             "data": "synthetic (splitmix64 records generated on device)",
-            "config": dict(cfg, parallelism=f"record-shard x{world}", kernels=lib.sg_build_info().decode()),
+            "config": dict(cfg, parallelism=f"record-shard x{world}", kernels=build,
+                           library=provenance),
             "roofline": {"bound": "hbm", "kernel": dom_kernel,
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
@@ -659,25 +841,26 @@ def main():
                          "hbm_read": {"achieved": round(achieved_read, 1), "frac": round(achieved_read / HBM_PEAK_GBS, 4),
                                       "alg_read_bytes_per_launch": alg_read[dom]}},
             "valu_roofline": valu,
+            "sclk_mhz": sclk,
+            "board_power_w": (mon.get("board_power_w") or {}).get("mean"),
+            "device_monitor": mon,
             "kernel_ms": {"seal": round(tm["seal_ms"], 4), "open": round(tm["open_ms"], 4),
                           "keying": round(tm["keying_ms"], 4), "sum_per_step": round(kernel_sum_ms, 4),
                           "sum_vs_step": round(kernel_sum_ms / ms_per_step, 4),
                           "launches": int(tm.get("n_seal", 0)) + int(tm.get("n_open", 0)),
                           "note": "HIP events on the launch stream over steps run right after the timed region"},
             "records_per_s": round((args.records if args.strong else count * world) * args.steps / elapsed, 1),
-            "correct": roundtrip_ok,
             "cpu_baseline": cpu,
         }
-        if exact is not None:
-            line.update(exact)
+        line.update(correctness_fields(correct, ranks, flags, exact))
         if scatter_gather is not None:
             line["scatter_gather"] = scatter_gather
         print(json.dumps(line), flush=True)
     if dist:
         dist.barrier()
         dist.destroy_process_group()
-    if not roundtrip_ok:
-        sys.exit(3)
+    if exit_code(correct):
+        sys.exit(exit_code(correct))
 
 
 if __name__ == "__main__":

@@ -57,7 +57,7 @@ def embedded_hash(lib: Path):
     import re
 
     try:
-        m = re.search(rb"sg-src:([0-9a-f]{16})", lib.read_bytes())
+        m = re.search(rb"sg-src:([0-9a-f]{16}(?:\+var:[A-Za-z0-9_.:-]+)?)", lib.read_bytes())
     except OSError:
         return None
     return m.group(1).decode() if m else None
@@ -92,6 +92,11 @@ def build_library(force: bool = False, out: Path | None = None, defines=()) -> P
     if defines and target.resolve() == LIB.resolve():
         raise ValueError("the product library is built without -D switches; pass out= for a variant")
     src = source_hash()
+    marker = src
+    if defines:  # a -D variant never carries the product's identity (see _native.load)
+        import hashlib
+
+        marker = f"{src}+var:defs:{hashlib.sha256(repr(tuple(defines)).encode()).hexdigest()[:8]}"
     if force or defines or _stale(target, HIP_DEPS) or embedded_hash(target) != src:
         import tempfile
         from concurrent.futures import ThreadPoolExecutor
@@ -101,7 +106,7 @@ def build_library(force: bool = False, out: Path | None = None, defines=()) -> P
         # fetch must not wait for its return right away (sg_wpr.hip)
         flags = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-mllvm",
                  "-amdgpu-atomic-optimizer-strategy=None", "-Wall", "-Wno-unused-result", *defines,
-                 f'-DSG_SOURCE_HASH="{src}"']
+                 f'-DSG_SOURCE_HASH="{marker}"']
         # one translation unit per compiler process (the kernels take most of a
         # minute each), then one link
         with tempfile.TemporaryDirectory(prefix="sg_build_") as td:

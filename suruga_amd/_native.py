@@ -99,6 +99,23 @@ _lib = None
 _lock = threading.Lock()
 
 
+def provenance_error(got: str, want: str, allow_variant: bool):
+    """None when a library embedding source marker `got` may run in a tree
+    whose sources hash to `want`, else the reason.  Experiment variants
+    (tools/build_variant.py, _build.build_library(defines=...)) embed
+    "<tree hash>+var:<name>:<edit hash>" and run only on explicit request
+    (SURUGA_ALLOW_VARIANT=1, as tools/ab_libs.sh sets)."""
+    if got == want:
+        return None
+    if got.startswith(want + "+var:"):
+        if allow_variant:
+            return None
+        return (f"is an experiment variant ({got}) of this tree: set SURUGA_ALLOW_VARIANT=1 to time it; "
+                "the product runs only the tree's own build")
+    return (f"was built from other sources (embedded hash {got}, tree {want}): "
+            "rebuild with `python -m suruga_amd._build`")
+
+
 def _declare(lib: C.CDLL) -> None:
     u8p = C.POINTER(C.c_uint8)
     lib.sg_key_size.restype = C.c_size_t
@@ -184,11 +201,22 @@ def load(path: Path | None = None) -> C.CDLL:
             from ._build import source_hash
 
             got, want = lib.sg_source_hash().decode(), source_hash()
-            if got != want:
-                raise ImportError(f"{p} was built from other sources (embedded hash {got}, tree {want}): "
-                                  "rebuild with `python -m suruga_amd._build`")
+            err = provenance_error(got, want, os.environ.get("SURUGA_ALLOW_VARIANT") == "1")
+            if err:
+                raise ImportError(f"{p} {err}")
+            global _lib_path
+            _lib_path = str(p.resolve())
             _lib = lib
         return _lib
+
+
+_lib_path = None
+
+
+def loaded_info() -> dict:
+    """Which library this process runs and the source hash it carries (bench provenance)."""
+    lib = load()
+    return {"path": _lib_path, "source_hash": lib.sg_source_hash().decode()}
 
 
 def last_error() -> str:

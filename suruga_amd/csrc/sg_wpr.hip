@@ -463,6 +463,13 @@ __device__ __forceinline__ uint64_t mad_i64_i32(int32_t a, uint32_t b, uint64_t 
     asm volatile("v_mad_i64_i32 %0, %1, %2, %3, %4" : "=&v"(d), "=s"(cc) : "v"(a), "s"(b), "v"(c));
     return d;
 }
+// a * b + c (unsigned 32 x 32 + 64 bits, b wave-uniform) in one v_mad_u64_u32
+// (a power-of-two b would otherwise become a 64-bit shift and an add)
+__device__ __forceinline__ uint64_t mad_u64_u32(uint32_t a, uint32_t b, uint64_t c) {
+    uint64_t d, cc;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=&v"(d), "=s"(cc) : "v"(a), "s"(b), "v"(c));
+    return d;
+}
 __device__ __forceinline__ uint64_t mad_i64_i32_1(int32_t a, uint64_t c) {
     uint64_t d, cc;
     asm volatile("v_mad_i64_i32 %0, %1, %2, 1, %3" : "=&v"(d), "=s"(cc) : "v"(a), "s"(c));
@@ -546,6 +553,31 @@ __device__ __forceinline__ void dma_sv(uint32_t l0, const void* sbase, uint32_t 
                  : "memory");
 }
 
+// Address forms of the output path (SG_WPR_ADDR, default on): the staged
+// output is read from LDS through one VGPR base (the lane's swizzled unit in
+// the wave's slice) with the buffer and piece as immediate offsets, and stored
+// with the saddr form of global_store (record base in SGPRs, the lane's 16-byte
+// offset in a VGPR, the piece as the instruction offset), so that no VALU
+// address arithmetic runs per piece.  The stores are asm: their vmcnt is
+// counted by the kernel's own waits like the DMAs' (s_nop: no VALU may
+// overwrite the data registers of a >64-bit store in the next cycle).
+#ifndef SG_WPR_ADDR
+#define SG_WPR_ADDR 1
+#endif
+// digit lines from the unreduced product limbs (round 4; 0: carry ripple first)
+#ifndef SG_WPR_DIGIT_MAD
+#define SG_WPR_DIGIT_MAD 1
+#endif
+typedef const __attribute__((address_space(3))) u32x4* lu128p;
+template <uint32_t OFF>
+__device__ __forceinline__ void gst16_s(const void* sbase, uint32_t voff, const u32x4& v) {
+    static_assert(OFF < 4096u, "global instruction offset");
+    asm volatile("global_store_dwordx4 %0, %1, %2 offset:%3" SG_DMA_POL "\n\ts_nop 0"
+                 :
+                 : "v"(voff), "v"(v), "s"(sbase), "i"(OFF)
+                 : "memory");
+}
+
 __device__ __forceinline__ void dma_one(uint32_t l0, const void* g) {
     uint32_t keep;
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
@@ -593,6 +625,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     uint32_t mac_lo_a = (uint32_t)(uintptr_t)(mac_base - 64), mac_hi_a = (uint32_t)(uintptr_t)(mac_base + 960 - 64);
     asm volatile("" : "+v"(mac_lo_a), "+v"(mac_hi_a));
     const lu32p mac_lo = (lu32p)(uintptr_t)mac_lo_a, mac_hi = (lu32p)(uintptr_t)mac_hi_a;
+    // output read-out base (the lane's swizzled unit of the wave's slice) and the
+    // lane's byte offset of a lane-contiguous 1 KiB piece (SG_WPR_ADDR)
+    // (uniform 16 KiB launches only: the bucket kernels have no VGPRs to spare)
+    constexpr bool kAddr = SG_WPR_ADDR && !LIST;
+    uint32_t ob_a = (uint32_t)(uintptr_t)(buf + 16u * wunit), lane16 = 16u * lane;
+    if constexpr (kAddr) asm volatile("" : "+v"(ob_a), "+v"(lane16));
+    const lu128p ob_base = (lu128p)(uintptr_t)ob_a;
     const uint32_t cnt = wl.count;
     const uint32_t ngroups = (cnt + kWprWaves - 1u) / kWprWaves;
 
@@ -780,16 +819,34 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
         }
         wave_lds_sync();  // every table read is done before the lines overwrite it
         if (lane < kWprLines) {
-            // any representative below 2^130 of r^e works (the MAC is exact mod p):
-            // the carry ripple suffices, no conditional subtraction of p
-            const F26 v = ripple_full(lv);
-            uint32_t c;  // digits = the bytes of v + 0x80..80, each ^ 0x80
+            // any representative below 2^135 of r^e works (the MAC is exact mod p),
+            // so the product's limbs (v0, v2..v4 < 2^26, v1 < 2^26 + 2^9) are
+            // summed straight into 32-bit words, X = sum v_i 2^(26 i) < 2^131:
+            // four v_mad_u64_u32, no carry ripple, no reduction (round 4; the
+            // ripple_full form took ~35 more VALU per record)
+            uint32_t c;  // digits = the bytes of X + 0x80..80, each ^ 0x80
             uint32_t d[5];
+#if !SG_WPR_DIGIT_MAD
+            const F26 v = ripple_full(lv);
             d[0] = addc(v.v0 | (v.v1 << 26), 0x80808080u, 0u, &c) ^ 0x80808080u;
             d[1] = addc((v.v1 >> 6) | (v.v2 << 20), 0x80808080u, c, &c) ^ 0x80808080u;
             d[2] = addc((v.v2 >> 12) | (v.v3 << 14), 0x80808080u, c, &c) ^ 0x80808080u;
             d[3] = addc((v.v3 >> 18) | (v.v4 << 8), 0x80808080u, c, &c) ^ 0x80808080u;
             d[4] = ((v.v4 >> 24) + 0x80u + c) ^ 0x80u;
+#else
+            uint64_t t = mad_u64_u32(lv.v1, 1u << 26, (uint64_t)lv.v0);
+            const uint32_t x0 = (uint32_t)t;
+            t = mad_u64_u32(lv.v2, 1u << 20, t >> 32);
+            const uint32_t x1 = (uint32_t)t;
+            t = mad_u64_u32(lv.v3, 1u << 14, t >> 32);
+            const uint32_t x2 = (uint32_t)t;
+            t = mad_u64_u32(lv.v4, 1u << 8, t >> 32);
+            d[0] = addc(x0, 0x80808080u, 0u, &c) ^ 0x80808080u;
+            d[1] = addc(x1, 0x80808080u, c, &c) ^ 0x80808080u;
+            d[2] = addc(x2, 0x80808080u, c, &c) ^ 0x80808080u;
+            d[3] = addc((uint32_t)t, 0x80808080u, c, &c) ^ 0x80808080u;
+            d[4] = ((uint32_t)(t >> 32) + 0x80u + c) ^ 0x80u;
+#endif
             uint8_t* ln = lines + kWprLineBytes * lane;
             const u32x4 z = zero4();
             if constexpr (TLS) {
@@ -964,9 +1021,23 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
             // piece k of the next chunk's DMA follows the store of output piece k
             // (the same LDS range): the stores and DMAs of the 16 waves of a CU
             // spread over five gaps instead of queueing behind each other.
-            auto out_piece = [&](uint32_t k) { return ld16(pb + 1024u * k + 16u * wunit); };
+            auto out_piece = [&](uint32_t k) {
+                if constexpr (kAddr) return ob_base[(kWprChunk * (bj ^ 1u) + 1024u * k) / 16u];
+                return ld16(pb + 1024u * k + 16u * wunit);
+            };
             auto store_piece = [&](uint32_t k, const u32x4& v) {
-                if (!LIST || 1024u * k + 16u * lane >= plo) gst16(pend_dst + 1024u * k + 16u * lane, v);
+                if (!LIST || 1024u * k + 16u * lane >= plo) {
+                    if constexpr (kAddr) {
+                        switch (k) {
+                            case 0: gst16_s<0u>(pend_dst, lane16, v); break;
+                            case 1: gst16_s<1024u>(pend_dst, lane16, v); break;
+                            case 2: gst16_s<2048u>(pend_dst, lane16, v); break;
+                            default: gst16_s<3072u>(pend_dst, lane16, v); break;
+                        }
+                    } else {
+                        gst16(pend_dst + 1024u * k + 16u * lane, v);
+                    }
+                }
             };
             auto dma_piece = [&](uint32_t k) {
                 const uint32_t ldsb = lds_wave + kWprChunk * (bj ^ 1u);

@@ -1,0 +1,127 @@
+"""GPU clock and board power during a timed region, from sysfs (plain file
+reads on a background thread, no subprocess, no GPU call).
+
+bench.py prices its issue-bound roofline (valu_roofline) at the shader clock
+the kernels actually ran at: MI355X sits at its board power cap under the C1
+load, well below the 2.4 GHz peak clock.  The amdgpu driver
+exposes, per card, hwmon `freq1_input` (sclk, Hz) and `power1_average` /
+`power1_input` (uW), and `pp_dpm_sclk` (DPM levels, the current one marked
+'*').  Whatever of these exists is sampled; missing files give None.
+"""
+from __future__ import annotations
+
+import glob
+import os
+import threading
+import time
+
+
+def _read(path):
+    try:
+        with open(path) as f:
+            return f.read()
+    except OSError:
+        return None
+
+
+def card_dirs():
+    """sysfs device directories of the amdgpu PCI functions (partition
+    platform devices, amdgpu_xcp_*, carry no hwmon and are skipped)."""
+    devs = []
+    for d in sorted(glob.glob("/sys/class/drm/card[0-9]*/device")):
+        real = os.path.realpath(d)
+        if real not in devs and (_read(os.path.join(d, "vendor")) or "").strip() == "0x1002" \
+                and glob.glob(os.path.join(d, "hwmon", "hwmon*")):
+            devs.append(real)
+    return devs
+
+
+def pick_card(pci_bus_id: str | None):
+    """(the card whose PCI address equals `pci_bus_id`, how it was chosen).
+    A node has several cards, most of them another job's: without an exact
+    match nothing is sampled unless exactly one card is visible."""
+    devs = card_dirs()
+    if pci_bus_id:
+        want = pci_bus_id.lower()
+        for d in devs:
+            if os.path.basename(d).lower() == want:
+                return d, "pci address match"
+    if len(devs) == 1:
+        return devs[0], "only card visible"
+    return None, f"no card with PCI address {pci_bus_id} among {len(devs)}"
+
+
+class Sampler:
+    """Samples sclk (MHz) and board power (W) of one card every `period` s
+    between start() and stop()."""
+
+    def __init__(self, pci_bus_id: str | None = None, period: float = 0.02):
+        self.period = period
+        self.dev = None
+        self.files = {}
+        self.pci_bus_id = pci_bus_id
+        d0, self.how = pick_card(pci_bus_id)
+        for d in ([d0] if d0 else []):
+            self.dev = d
+            for hw in sorted(glob.glob(os.path.join(d, "hwmon", "hwmon*"))):
+                for key, name in (("sclk_hz", "freq1_input"), ("power_uw", "power1_average"),
+                                  ("power_uw_in", "power1_input")):
+                    p = os.path.join(hw, name)
+                    if key not in self.files and os.path.exists(p):
+                        self.files[key] = p
+            if os.path.exists(os.path.join(d, "pp_dpm_sclk")):
+                self.files["dpm"] = os.path.join(d, "pp_dpm_sclk")
+        self.samples = []
+        self._stop = threading.Event()
+        self._th = None
+
+    def _one(self):
+        s = {"t": time.perf_counter()}
+        v = _read(self.files["sclk_hz"]) if "sclk_hz" in self.files else None
+        if v and v.strip().isdigit():
+            s["sclk_mhz"] = int(v) / 1e6
+        elif "dpm" in self.files:
+            for line in (_read(self.files["dpm"]) or "").splitlines():
+                if line.strip().endswith("*"):
+                    try:
+                        s["sclk_mhz"] = float(line.split(":")[1].strip().rstrip("*").strip().lower().rstrip("mhz"))
+                    except (IndexError, ValueError):
+                        pass
+        for key in ("power_uw", "power_uw_in"):
+            v = _read(self.files[key]) if key in self.files else None
+            if v and v.strip().isdigit():
+                s["power_w"] = int(v) / 1e6
+                break
+        return s
+
+    def _run(self):
+        while not self._stop.is_set():
+            self.samples.append(self._one())
+            self._stop.wait(self.period)
+
+    def start(self):
+        if self.files:
+            self._th = threading.Thread(target=self._run, daemon=True)
+            self._th.start()
+        return self
+
+    def stop(self):
+        self._stop.set()
+        if self._th:
+            self._th.join()
+        return self.summary()
+
+    def summary(self):
+        def stats(key):
+            v = [s[key] for s in self.samples if key in s]
+            if not v:
+                return None
+            # drop the first and last tenth (ramps at the edges of the region)
+            k = len(v) // 10
+            core = v[k:len(v) - k] or v
+            return {"mean": round(sum(core) / len(core), 1), "min": round(min(core), 1), "max": round(max(core), 1),
+                    "samples": len(v)}
+
+        return {"card": self.dev, "pci_bus_id": self.pci_bus_id, "chosen_by": self.how,
+                "sources": {k: os.path.basename(v) for k, v in self.files.items()},
+                "sclk_mhz": stats("sclk_mhz"), "board_power_w": stats("power_w")}

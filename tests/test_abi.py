@@ -260,3 +260,18 @@ def test_no_kernel_uses_scratch(tmp_path, lib):
             assert sz == 0, f"{nm} uses {sz} bytes of scratch"
         seen += len(names)
     assert seen >= 20
+
+
+def test_variant_marker_needs_explicit_opt_in():
+    """ADVICE r3: experiment variants embed "<tree hash>+var:<name>:<edit hash>";
+    the loader refuses them unless SURUGA_ALLOW_VARIANT=1, and refuses any other
+    hash outright."""
+    from suruga_amd._native import provenance_error
+
+    want = "0123456789abcdef"
+    assert provenance_error(want, want, False) is None
+    var = want + "+var:pk_nomac:1a2b3c4d"
+    assert "SURUGA_ALLOW_VARIANT" in provenance_error(var, want, False)
+    assert provenance_error(var, want, True) is None
+    assert "other sources" in provenance_error("fedcba9876543210", want, True)
+    assert "other sources" in provenance_error("fedcba9876543210+var:x:00", want, True)

@@ -90,3 +90,97 @@ def test_bench_gpus_two_launches_its_own_ranks(gpu):
     assert j["n_gpus"] == 2 and j["correct"] and j["scaling"] == "weak"
     assert j["records_per_s"] * j["ms_per_step"] / 1e3 == pytest.approx(8192, rel=1e-3)
     assert j["scatter_gather"]["verified"]
+
+
+def _verdict_worker(rank, world, port, q):
+    """Each rank seals its records with the oracle (standing in for the GPU),
+    checks the XOR-fold of its tags against the oracle's fold as bench.py does;
+    rank 1 corrupts one tag first.  bench.rank_verdict ANDs the ranks."""
+    import torch.distributed as dist
+
+    sys.path.insert(0, str(ROOT))
+    import bench
+    from oracle_ffi import oracle as get_oracle
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        o, n, key = get_oracle(), 256, bytes(range(32))
+        tags = []
+        for i in range(rank * 4, rank * 4 + 4):
+            ct = o.seal(key, i.to_bytes(8, "big"), o.fill_record(0x53555255, i, n), o.tls_ad(i, n))
+            tags.append(bytearray(ct[n:]))
+        if rank == 1:
+            tags[2][5] ^= 0x01  # one corrupted tag on rank 1
+        fold = bytes(a ^ b ^ c ^ d for a, b, c, d in zip(*tags))
+        exact = {"bitexact_fold": fold == o.tag_fold_tls(key, rank * 4, 0x53555255, rank * 4, n, 4, 1),
+                 "bitexact_sample": True}
+        mine = {"rank": rank, "local_rank": rank, "device": 0, "roundtrip_ok": True, **exact}
+        correct, ranks, flags = bench.rank_verdict(dist, mine)
+        line = bench.correctness_fields(correct, ranks, flags, exact) if rank == 0 else None
+        q.put((rank, line, bench.exit_code(correct)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_correct_is_and_over_ranks_gloo():
+    """a corrupted tag on rank 1 makes rank 0's line say
+    "correct": false (and that rank's flag false), and every rank exits 3."""
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    mp.start_processes(_verdict_worker, args=(2, _port(), q), nprocs=2, join=True, start_method="spawn")
+    res = {r: (line, rc) for r, line, rc in (q.get(timeout=60) for _ in range(2))}
+    line, rc0 = res[0]
+    assert line["correct"] is False and line["bitexact_fold"] is False
+    assert [r["bitexact_fold"] for r in line["ranks"]] == [True, False]
+    assert rc0 == 3 and res[1][1] == 3
+
+
+@pytest.mark.gpu
+def test_bench_failing_rank_fails_the_line(gpu):
+    """The real bench path: two gloo ranks on the test box's card, rank 1's
+    bit-exactness check forced to fail (SG_BENCH_CORRUPT_RANK=1): rank 0 prints
+    "correct": false and the run exits non-zero."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(SG_DIST_BACKEND="gloo", SG_BENCH_CORRUPT_RANK="1")
+    p = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--records", "4096", "--steps", "2",
+                        "--warmup", "1", "--no-cpu-baseline", "--sg-records", "0"], capture_output=True, text=True,
+                       timeout=300, cwd=ROOT, env=env)
+    assert p.returncode != 0
+    j = _last_json(p.stdout)
+    assert j["correct"] is False and j["bitexact_fold"] is False
+    assert [r["rank"] for r in j["ranks"]] == [0, 1] and j["ranks"][0]["bitexact_fold"] is True
+
+
+@pytest.mark.gpu
+def test_bench_local_rank_maps_to_visible_device(gpu):
+    """LOCAL_RANK=1 on a one-GPU box runs on device 1 mod 1 = 0, and the line
+    names the device each rank used."""
+    import torch
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "MASTER_PORT")}
+    env["LOCAL_RANK"] = "1"
+    p = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--records", "4096", "--steps", "2", "--warmup", "1",
+                        "--no-cpu-baseline"], capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    j = _last_json(p.stdout)
+    nd = torch.cuda.device_count()
+    assert j["correct"] and j["ranks"][0]["local_rank"] == 1 and j["ranks"][0]["device"] == 1 % nd
+
+
+@pytest.mark.gpu
+def test_bench_c2_two_ranks_scatter_gather(gpu):
+    """--workload c2 at N=2 (gloo, one card): the byte-balanced scatter ->
+    per-rank mixed seal -> gather round trip is timed and verified."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["SG_DIST_BACKEND"] = "gloo"
+    p = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--workload", "c2", "--records", "8192",
+                        "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--sg-records", "1024"],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    j = _last_json(p.stdout)
+    sg = j["scatter_gather"]
+    assert j["correct"] and sg["verified"] and sg["split"] == "byte_balanced_ranges" and sg["records"] == 2048
+    assert sg["ranges"][0][0] == 0 and sg["ranges"][-1][1] == 2048

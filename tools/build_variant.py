@@ -5,8 +5,10 @@ sources into ablib/<name>.so (same-box A/B with tools/ab_libs.sh).
 The product sources are never modified: the csrc/ tree is copied to a
 temporary directory, the edits of an edit file are applied there (each edit
 must match exactly once), and the copy is compiled with the product flags and
-the tree's source hash (so that _native.load() accepts the variant when it is
-named by SURUGA_GPU_LIB).  Timing-only variants (skipped work, wrong output)
+the marker "<tree hash>+var:<name>:<hash of the edits and defines>", so that
+a variant never carries the product's identity: _native.load() accepts it
+(named by SURUGA_GPU_LIB) only with SURUGA_ALLOW_VARIANT=1, and bench.py
+prints the loaded library's path and marker in its line.  Timing-only variants (skipped work, wrong output)
 live only in ablib/ and in the edit files under tools/variants/.
 
 Usage: python tools/build_variant.py <name> <edits.py> [-DNAME=V ...]
@@ -44,9 +46,13 @@ def main() -> None:
                 raise SystemExit(f"edit matches {n} times in {fname}: {old[:60]!r}")
             f.write_text(txt.replace(old, new))
         srcs = [tdp / "pkg" / "csrc" / p.name for p in _build.HIP_SOURCES]
+        import hashlib
+
+        eh = hashlib.sha256(repr((edits, defines)).encode()).hexdigest()[:8]
+        marker = f"{_build.source_hash()}+var:{name}:{eh}"
         flags = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-mllvm",
                  "-amdgpu-atomic-optimizer-strategy=None", "-Wall", "-Wno-unused-result", f"-I{tdp / 'include'}",
-                 *defines, f'-DSG_SOURCE_HASH="{_build.source_hash()}"']
+                 *defines, f'-DSG_SOURCE_HASH="{marker}"']
         objs = [tdp / f"{s.stem}.o" for s in srcs]
 
         def cc(so):
