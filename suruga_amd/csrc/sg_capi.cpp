@@ -449,6 +449,8 @@ static int single(sg_ctx* c, bool open, const uint8_t* nonce, size_t nonce_len, 
     b.stream = c->stream;
     b.workspace = c->d_ws;
     b.workspace_size = sg_workspace_size(1);
+    // a failed open's plaintext is withheld on the host below: no device scrub
+    b.flags = open ? SG_BATCH_KEEP_FAILED : 0u;
     int rc = open ? sg_open_batch(&b) : sg_seal_batch(&b);
     if (rc != SG_OK) return rc;
     const size_t out_len = open ? n : n + SG_MAC_LEN;

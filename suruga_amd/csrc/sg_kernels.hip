@@ -679,6 +679,11 @@ __global__ __launch_bounds__(256) void sg_compare_kernel(const uint8_t* a, uint6
 // kernels, by the wave that finds it.  Records that failed are rare, so the
 // launch costs one status byte per record when none did.  Status 2 (too
 // short) has no output and status 3 (longer than max_len) was never written.
+// Each wave scans 64 statuses and zeroes the output of every failed record in
+// its ballot with the whole wave: byte stores up to the first 16-byte boundary,
+// then 16-byte stores (1 KiB per wave instruction), then the byte tail
+// (one byte per lane made a batch of failed 16 KiB records cost more
+// than the AEAD launch itself).
 __global__ __launch_bounds__(256) void sg_scrub_kernel(const KParams p) {
     const uint32_t base = blockIdx.x * 256u + (threadIdx.x & ~63u), lane = threadIdx.x & 63u;
     const uint32_t i = base + lane;
@@ -689,7 +694,14 @@ __global__ __launch_bounds__(256) void sg_scrub_kernel(const KParams p) {
         const uint32_t len = record_len(p, rec);
         const uint32_t n = len >= 16u ? len - 16u : 0u;
         uint8_t* o = p.out + (p.out_off ? p.out_off[rec] : p.out_stride * rec);
-        for (uint32_t b = lane; b < n; b += 64u) o[b] = 0u;
+        const uint32_t head = (uint32_t)((16u - ((uintptr_t)o & 15u)) & 15u);
+        const uint32_t h = head < n ? head : n;
+        if (lane < h) o[lane] = 0u;
+        const uint32_t nv = (n - h) >> 4;  // whole 16-byte units after the head
+        u32x4* ov = reinterpret_cast<u32x4*>(o + h);
+        for (uint32_t v = lane; v < nv; v += 64u) ov[v] = u32x4{0u, 0u, 0u, 0u};
+        const uint32_t t0 = h + 16u * nv;
+        if (t0 + lane < n) o[t0 + lane] = 0u;
     }
 }
 

@@ -50,6 +50,27 @@
 #include "sg_device.h"
 #include "sg_chacha_grp.inc"  // grouped ChaCha20 double round (tools/gen_chacha_grp.py --product)
 
+// Barriers per double round of the grouped asm (generated next to the macro)
+// and a compile-time count of the macro text itself: the idle waves of a
+// packed round execute exactly ten double rounds' worth of s_barrier.
+#define SG_PACK_XSTR(x) #x
+#define SG_PACK_STR(x) SG_PACK_XSTR(x)
+#define SG_PACK_IDLE_BARS (10 * SG_CHACHA_DR_NB1_BAR1_BARRIERS)
+namespace {
+constexpr unsigned count_barriers(const char* s) {
+    unsigned n = 0;
+    for (; *s; ++s) {
+        const char* b = "s_barrier";
+        const char* t = s;
+        while (*b && *t == *b) ++t, ++b;
+        if (!*b) ++n;
+    }
+    return n;
+}
+static_assert(count_barriers(SG_CHACHA_DR_NB1_BAR1) == SG_CHACHA_DR_NB1_BAR1_BARRIERS,
+              "barrier count of the double-round asm");
+}  // namespace
+
 #include <stdint.h>
 #include <stdlib.h>
 
@@ -298,7 +319,9 @@ __global__ __launch_bounds__(kPackThreads) void sg_pack_kernel(const KParams p, 
     // no chunk for it, so that all waves meet the same barriers.
     SG_STAMP(0u, 2);
     SG_STAMP(7u, 6);
-    const uint32_t total = L.total, nchunks = L.nchunks;
+    // (scalar: the idle-round branch below must be wave-uniform, or working and
+    // idle waves would meet different barrier counts)
+    const uint32_t total = L.total, nchunks = __builtin_amdgcn_readfirstlane(L.nchunks);
     const uint32_t nrounds = (nchunks + kPackWaves - 1u) / kPackWaves;
     // Chunk order within a round: SIMD pairs first (waves w and w + 4 share a
     // SIMD), so that in the last, partial round the chunks go to whole pairs
@@ -310,7 +333,8 @@ __global__ __launch_bounds__(kPackThreads) void sg_pack_kernel(const KParams p, 
     for (uint32_t k = 0; k < nrounds; ++k) {
         const uint32_t c = kPackWaves * k + (SG_PACK_IDLE_BARRIERS ? pos : wave);
         if (SG_PACK_IDLE_BARRIERS && c >= nchunks) {  // (wave-uniform) no chunk in this round
-            asm volatile(".rept 80\ns_barrier\n.endr" ::: "memory");  // 10 double rounds x 8 (sg_chacha_grp.inc)
+            // as many barriers as the ten double rounds of a working wave
+            asm volatile(".rept " SG_PACK_STR(SG_PACK_IDLE_BARS) "\ns_barrier\n.endr" ::: "memory");
             continue;
         }
         const uint32_t b = 64u * c + lane;

@@ -504,6 +504,9 @@ int sg_read_records(sg_ctx* c, uint64_t seq0, const uint8_t* wire, size_t wire_l
             b.stream = s.st;
             b.workspace = s.d_ws;
             b.workspace_size = sg_workspace_size(kChunk);
+            // the reader delivers nothing from a failed record (it stops there):
+            // no device scrub of failed records' output
+            b.flags = SG_BATCH_KEEP_FAILED;
             if ((rc = sg_open_batch(&b)) != SG_OK) return rc;
             SG_HIP(hipEventRecord(s.ev[2], s.st));
             SG_HIP(hipMemcpyAsync(s.h_out, s.d_out, (size_t)k * kSlot, hipMemcpyDeviceToHost, s.st));
