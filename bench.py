@@ -458,12 +458,15 @@ def issue_roofline(dom, workload, count, cus, dom_ms, tj, isa, sclk_mhz):
     """The dominant launch against its VALU issue bound at the clock it ran at
     (VERDICT r3 item 2).  Model (profiles/r01_valu_issue_probes.md): a wave64
     VALU instruction costs 2 SIMD clocks when it is a v_add / v_xor of the
-    lock-step ARX asm (paired with its SIMD partner wave), 4 otherwise
-    (rotates, every non-ARX instruction).  Instruction counts: the PMC
+    lock-step ARX asm or any other full-rate opcode (paired with its SIMD
+    partner wave), 4 otherwise (rotates and every half-rate instruction).  Instruction counts: the PMC
     SQ_INSTS_VALU of this build's profile (tj, per launch) split by the static
     census of the same sources (isa: tools/isa_census.py).  bound_ms = issue
     clocks per SIMD / sclk; frac = bound_ms / measured launch time (<= 1 when
-    the model holds: the rest is stalls, barriers and launch tails)."""
+    the model holds: the rest is stalls, barriers and launch tails).
+    Full-rate opcodes outside the asm are priced at 2 as well: the measured
+    cost of the feed-forward (124 v_add/v_xor per record, profiles/r04_ab:
+    -1.5 % when removed) is the paired rate, not 4."""
     if not isa or not sclk_mhz:
         return {"bound": "valu", "unavailable": "no ISA census of this build" if not isa else "no sclk reading"}
     kern = isa["kernels"]
@@ -478,10 +481,13 @@ def issue_roofline(dom, workload, count, cus, dom_ms, tj, isa, sclk_mhz):
         src = "PMC SQ_INSTS_VALU per record (profile of this build)" if vpr else "static census (no PMC profile)"
         vpr = vpr or k["valu"]
         arx = k["arx_full"] + k["arx_rot"]
-        clk_rec = 2 * k["arx_full"] + 4 * k["arx_rot"] + 4 * max(vpr - arx, 0.0)
+        oth = max(vpr - arx, 0.0)  # dynamic non-ARX VALU, split like the static census
+        full_share = k["other_full"] / k["other_valu"] if k.get("other_valu") else 0.0
+        clk_rec = 2 * k["arx_full"] + 4 * k["arx_rot"] + oth * (2 * full_share + 4 * (1 - full_share))
         clk = clk_rec * count / simds
         per = {"valu_per_record": round(vpr, 1), "arx_full_per_record": k["arx_full"],
-               "arx_rot_per_record": k["arx_rot"], "other_valu_per_record": round(max(vpr - arx, 0.0), 1),
+               "arx_rot_per_record": k["arx_rot"], "other_valu_per_record": round(oth, 1),
+               "other_full_rate_share": round(full_share, 3),
                "issue_clk_per_record": round(clk_rec, 1), "valu_source": src}
     else:
         byk = (tj or {}).get(f"{dom}_valu_by_kernel")
@@ -490,11 +496,12 @@ def issue_roofline(dom, workload, count, cus, dom_ms, tj, isa, sclk_mhz):
         clk, per, miss = 0.0, {}, []
         for name, v in byk.items():
             k = kern.get(name)
-            if k is None or not k.get("clk_per_valu"):
+            cpv = (k or {}).get("clk_per_valu_whole") or (k or {}).get("clk_per_valu")
+            if not cpv:
                 miss.append(name)
                 continue
-            clk += v * k["clk_per_valu"] / simds
-            per[name] = {"valu": round(v), "clk_per_valu": k["clk_per_valu"]}
+            clk += v * cpv / simds
+            per[name] = {"valu": round(v), "clk_per_valu": cpv}
         per = {"kernels": per, "not_in_census": miss,
                "valu_source": "PMC SQ_INSTS_VALU per kernel and batch, priced with each kernel's static mix"}
     bound_ms = clk / (sclk_mhz * 1e3)
@@ -716,18 +723,20 @@ def main():
         B.N.check(lib.sg_open_batch(C.byref(open_c)))
 
     torch.cuda.synchronize()  # inputs and tables made on the default stream
-    for _ in range(args.warmup):
-        step()
-    # the shader clock and board power over the timed region (sysfs, plain reads
-    # on a background thread): the issue-bound roofline is priced at this clock
+    # the shader clock and board power (sysfs, plain reads on a background
+    # thread from the warm-up to the end of the event-timed steps below): the
+    # issue-bound roofline is priced at the mean clock of the timed region
     from suruga_amd import devmon
 
     props = torch.cuda.get_device_properties(dev)
     bus = f"{props.pci_domain_id:04x}:{props.pci_bus_id:02x}:{props.pci_device_id:02x}.0"
     sampler = devmon.Sampler(bus).start()
+    for _ in range(args.warmup):
+        step()
+    t_region0 = time.perf_counter()
     elapsed = shard.timed(dist, step, args.steps, sync=torch.cuda.synchronize,
                           device=dev if backend == "nccl" else None)
-    mon = sampler.stop()
+    t_region1 = time.perf_counter()
 
     # per-kernel device time with HIP events on the launch stream, right after
     # the timed steps while the GPU is still at its steady-state clock (round 2
@@ -737,6 +746,7 @@ def main():
         step()
     tm = B.timing_read()
     B.set_timing(False)
+    mon = sampler.stop(t_region0, t_region1)
 
     # correctness of the last step (outside the timed region): every record
     # round-trips, and every tag and a sample of records equal the oracle's;
@@ -842,7 +852,7 @@ def main():
                                       "alg_read_bytes_per_launch": alg_read[dom]}},
             "valu_roofline": valu,
             "sclk_mhz": sclk,
-            "board_power_w": (mon.get("board_power_w") or {}).get("mean"),
+            "board_power_w": (mon.get("board_power_w") or {}).get("last"),
             "device_monitor": mon,
             "kernel_ms": {"seal": round(tm["seal_ms"], 4), "open": round(tm["open_ms"], 4),
                           "keying": round(tm["keying_ms"], 4), "sum_per_step": round(kernel_sum_ms, 4),

@@ -59,8 +59,11 @@ extern "C" {
 #define SG_NONCE_LEN        8u
 #define SG_MAC_LEN         16u
 #define SG_MAX_AD_LEN     255u
-/* One record is one workgroup and its ciphertext is staged in LDS for the
- * MAC.  TLS records are at most 2^14 (+2048 expansion) bytes (tls.rs:32-35). */
+/* The size-class kernels (every batch that is not uniform 16 KiB records or
+ * a mixed TLS batch of 64-byte multiples) stage a record's MAC stream in LDS,
+ * which bounds a record at 32 KiB; the wave-per-record and packed kernels
+ * stream their records.  TLS records are at most 2^14 (+2048 expansion) bytes
+ * (tls.rs:32-35). */
 #define SG_MAX_RECORD_LEN 32768u
 
 /* ---- Aead constants (chacha20_poly1305.rs:15-17, 104-119) --------------- */
@@ -307,8 +310,9 @@ int sg_set_lockstep(int enable);
 
 /* Kernel form for the small records of mixed TLS batches (64 B .. 4 KiB, a
  * multiple of 64 bytes, 16-byte aligned; C2): 1 = the packed kernel (the
- * 64-byte blocks of 64 consecutive records laid end to end over the lanes,
- * keyed in the same kernel), 0 = the size-class kernels.  Both are
+ * 64-byte blocks of runs of 128 records of the packed list laid end to end
+ * over the lanes of a 512-thread workgroup, keyed in the same kernel), 0 = the
+ * size-class kernels.  Both are
  * bit-exact; A/B and test switch like sg_set_lockstep.  Initial value:
  * environment SG_PACK ("0"/"1"), else 1.  Returns the previous setting; a
  * negative argument only queries. */

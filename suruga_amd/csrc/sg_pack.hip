@@ -116,10 +116,18 @@ constexpr uint32_t kSCtot = 22;   // constant term (5 limbs)
 constexpr uint32_t kSNb = 27, kSStart = 28, kSRec = 29;
 static_assert(kSRec < kSlotWords, "slot layout");
 
+// Per-record MAC accumulator (SG_PACK_ACC64, default on): the lane terms
+// fmul(Q, W) go in unreduced -- limbs 0, 2, 3, 4 < 2^26 (64 of them stay below
+// 2^32), limb 1 < 2^26 + 2^7 summed as 64 bits (ds_add_u64) -- instead of
+// through a full carry ripple per lane (~30 VALU per chunk; round 4).
+#ifndef SG_PACK_ACC64
+#define SG_PACK_ACC64 1
+#endif
+constexpr uint32_t kAccWords = SG_PACK_ACC64 ? 6u : 5u;  // v0 v2 v3 v4 | v1 (u64)  or  v0..v4
 struct PackLds {
     uint32_t slot[kPackRecs * kSlotWords];
     uint32_t tab[kPackRecs * kTabWords];
-    uint32_t acc[kPackRecs * 5];
+    alignas(8) uint32_t acc[kPackRecs * kAccWords];
     uint32_t bits[kPackBlocks / 32];  // run block b starts a record
     uint32_t base[kPackChunks];       // first-chunk histogram, then records starting before chunk c
     uint32_t wtot;                    // wave 0's blocks (setup scan)
@@ -210,7 +218,7 @@ __global__ __launch_bounds__(kPackThreads) void sg_pack_kernel(const KParams p, 
 
     SG_STAMP(0u, 0);
     for (uint32_t i = tid; i < kPackBlocks / 32u; i += kPackThreads) L.bits[i] = 0u;
-    for (uint32_t i = tid; i < kPackRecs * 5u; i += kPackThreads) L.acc[i] = 0u;
+    for (uint32_t i = tid; i < kPackRecs * kAccWords; i += kPackThreads) L.acc[i] = 0u;
     if (tid < kPackChunks) L.base[tid] = 0u;
 
     // ---- setup: lane m of waves 0-1 keys record m of the run ---------------------
@@ -400,13 +408,22 @@ __global__ __launch_bounds__(kPackThreads) void sg_pack_kernel(const KParams p, 
             const uint32_t i = sl[kSNb] - 1u - j;
             const uint32_t* tb = L.tab + m * kTabWords;
             const F26 W = tab_weight(tb, i);
-            const F26 t = ripple_full(fmul(Q, W));
-            uint32_t* ac = L.acc + 5u * m;
-            atomicAdd(ac + 0, t.v0);
-            atomicAdd(ac + 1, t.v1);
-            atomicAdd(ac + 2, t.v2);
-            atomicAdd(ac + 3, t.v3);
-            atomicAdd(ac + 4, t.v4);
+            uint32_t* ac = L.acc + kAccWords * m;
+            if constexpr (SG_PACK_ACC64) {
+                const F26 t = fmul(Q, W);
+                atomicAdd(ac + 0, t.v0);
+                atomicAdd(ac + 1, t.v2);
+                atomicAdd(ac + 2, t.v3);
+                atomicAdd(ac + 3, t.v4);
+                atomicAdd(reinterpret_cast<unsigned long long*>(ac + 4), (unsigned long long)t.v1);
+            } else {
+                const F26 t = ripple_full(fmul(Q, W));
+                atomicAdd(ac + 0, t.v0);
+                atomicAdd(ac + 1, t.v1);
+                atomicAdd(ac + 2, t.v2);
+                atomicAdd(ac + 3, t.v3);
+                atomicAdd(ac + 4, t.v4);
+            }
         }
     }
     SG_STAMP(0u, 3);
@@ -418,8 +435,10 @@ __global__ __launch_bounds__(kPackThreads) void sg_pack_kernel(const KParams p, 
     if (act) {
         const uint32_t* sl = L.slot + m0 * kSlotWords;
         const uint32_t n = 64u * sl[kSNb], rec = sl[kSRec];
-        const uint32_t* ac = L.acc + 5u * m0;
-        F26 f = carry1(F26{ac[0], ac[1], ac[2], ac[3], ac[4]});
+        const uint32_t* ac = L.acc + kAccWords * m0;
+        // (ACC64: v1 = lo + hi 2^32 -> hi 2^58 = (hi << 6) 2^52 joins limb 2)
+        F26 f = SG_PACK_ACC64 ? carry1(F26{ac[0], ac[4], ac[1] + (ac[5] << 6), ac[2], ac[3]})
+                              : carry1(F26{ac[0], ac[1], ac[2], ac[3], ac[4]});
         f = carry1(f26_add(f, load_f26(sl + kSCtot)));
         const uint32_t s[4] = {sl[kSS + 0], sl[kSS + 1], sl[kSS + 2], sl[kSS + 3]};
         uint32_t tw[4];

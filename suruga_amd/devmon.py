@@ -55,10 +55,11 @@ class Sampler:
     """Samples sclk (MHz) and board power (W) of one card every `period` s
     between start() and stop()."""
 
-    def __init__(self, pci_bus_id: str | None = None, period: float = 0.02):
+    def __init__(self, pci_bus_id: str | None = None, period: float = 0.005):
         self.period = period
         self.dev = None
         self.files = {}
+        self.static = {}
         self.pci_bus_id = pci_bus_id
         d0, self.how = pick_card(pci_bus_id)
         for d in ([d0] if d0 else []):
@@ -71,6 +72,12 @@ class Sampler:
                         self.files[key] = p
             if os.path.exists(os.path.join(d, "pp_dpm_sclk")):
                 self.files["dpm"] = os.path.join(d, "pp_dpm_sclk")
+            for hw in sorted(glob.glob(os.path.join(d, "hwmon", "hwmon*"))):
+                for key, name in (("power_cap_w", "power1_cap"), ("power_label", "power1_label")):
+                    v = _read(os.path.join(hw, name))
+                    if v is not None and key not in self.static:
+                        v = v.strip()
+                        self.static[key] = int(v) / 1e6 if v.isdigit() else v
         self.samples = []
         self._stop = threading.Event()
         self._th = None
@@ -105,15 +112,23 @@ class Sampler:
             self._th.start()
         return self
 
-    def stop(self):
+    def stop(self, t0=None, t1=None):
         self._stop.set()
         if self._th:
             self._th.join()
-        return self.summary()
+        return self.summary(t0, t1)
 
-    def summary(self):
-        def stats(key):
-            v = [s[key] for s in self.samples if key in s]
+    def summary(self, t0=None, t1=None):
+        """sclk: the samples taken in [t0, t1] (perf_counter; the timed region),
+        its ramps at the edges dropped.  Power: the driver's power1_input is a
+        running average over a window longer than a short timed region (it
+        climbs from the idle value through the run), so the line reports its
+        last value and maximum over the whole sampled span next to the
+        region's mean."""
+        inside = [s for s in self.samples if (t0 is None or s["t"] >= t0) and (t1 is None or s["t"] <= t1)]
+
+        def stats(key, rows):
+            v = [s[key] for s in rows if key in s]
             if not v:
                 return None
             # drop the first and last tenth (ramps at the edges of the region)
@@ -122,6 +137,11 @@ class Sampler:
             return {"mean": round(sum(core) / len(core), 1), "min": round(min(core), 1), "max": round(max(core), 1),
                     "samples": len(v)}
 
+        pw = [s["power_w"] for s in self.samples if "power_w" in s]
+        power = stats("power_w", inside)
+        if power is not None and pw:
+            power.update({"last": round(pw[-1], 1), "max_overall": round(max(pw), 1)})
         return {"card": self.dev, "pci_bus_id": self.pci_bus_id, "chosen_by": self.how,
                 "sources": {k: os.path.basename(v) for k, v in self.files.items()},
-                "sclk_mhz": stats("sclk_mhz"), "board_power_w": stats("power_w")}
+                "sclk_mhz": stats("sclk_mhz", inside), "board_power_w": power, **self.static,
+                "period_s": self.period}

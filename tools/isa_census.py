@@ -10,10 +10,14 @@ kernel (rocprofv3's demangled name):
   arx_full / arx_rot   VALU inside the generated double-round asm
                        (v_add/v_xor pair at 2 clocks in lock-step, v_alignbit
                        at 4: profiles/r01_valu_issue_probes.md)
-  other_valu           every other VALU of the census (static, all paths)
+  other_valu           every other VALU of the census (static, all paths),
+                       split into other_full (full-rate opcodes: add, xor,
+                       and, or, mov, right shifts, bitop3) and other_half
   mfma, lds, vmem, salu
   clk_per_valu         the issue model's clocks per VALU instruction of this
-                       mix: (2 arx_full + 4 arx_rot + 4 other) / (all VALU)
+                       mix: full-rate opcodes 2 (paired with the SIMD's other
+                       lock-step wave, as the FF A/B of profiles/r04_ab shows
+                       outside the asm too), every other VALU 4
 
 bench.py prices the PMC-counted dynamic VALU of a launch with clk_per_valu
 (valu_roofline), and DESIGN.md §4.2's ISA table is this file's C1 entry.
@@ -61,12 +65,25 @@ def census_file(path: Path):
         af = sum(v for k, v in arx.items() if k in FULL)
         ar = sum(arx.values()) - af
         oth = sum(other.values())
+        oth_full = sum(v for k, v in other.items() if k.split("_e32")[0].split("_e64")[0] in FULL)
         tot = af + ar + oth
         out[dem] = {"scope": "record loop" if looped else "whole kernel", "arx_full": af, "arx_rot": ar,
-                    "other_valu": oth, "valu": tot, "mfma": kinds.get("mfma", 0), "lds": kinds.get("lds", 0),
+                    "other_valu": oth, "other_full": oth_full, "other_half": oth - oth_full, "valu": tot,
+                    "mfma": kinds.get("mfma", 0), "lds": kinds.get("lds", 0),
                     "vmem": kinds.get("vmem", 0), "salu": kinds.get("salu", 0),
-                    "clk_per_valu": round((2 * af + 4 * ar + 4 * oth) / tot, 4) if tot else None,
-                    "other_by_op": dict(other.most_common(12))}
+                    "clk_per_valu": round((2 * (af + oth_full) + 4 * (ar + oth - oth_full)) / tot, 4) if tot else None,
+                    "other_by_op": dict(other.most_common(16))}
+        # the whole function's mix (setup and tails included): what bench.py
+        # prices a kernel's PMC-counted VALU with (a loop region of a kernel
+        # with a complex CFG need not hold all of its per-iteration code)
+        warx, woth, _, _ = ic.census(body_all)
+        waf = sum(v for k, v in warx.items() if k in FULL)
+        war = sum(warx.values()) - waf
+        wof = sum(v for k, v in woth.items() if k.split("_e32")[0].split("_e64")[0] in FULL)
+        wtot = waf + war + sum(woth.values())
+        out[dem]["whole"] = {"arx_full": waf, "arx_rot": war, "other_full": wof,
+                             "other_half": sum(woth.values()) - wof, "valu": wtot}
+        out[dem]["clk_per_valu_whole"] = round((2 * (waf + wof) + 4 * (wtot - waf - wof)) / wtot, 4) if wtot else None
     return out
 
 
@@ -85,15 +102,16 @@ def main():
             subprocess.run([_build.hipcc(), *flags, "-c", "-o", str(wd / f"{s.stem}.o"), str(s)], cwd=wd, check=True,
                            capture_output=True)
             kernels.update(census_file(wd / f"{s.stem}-hip-amdgcn-amd-amdhsa-gfx950.s"))
-    res = {"source_hash": src, "model": "clocks per wave64 VALU: v_add/v_xor of the lock-step ARX asm 2, every "
-                                        "rotate and every other VALU 4 (profiles/r01_valu_issue_probes.md)",
+    res = {"source_hash": src, "model": "clocks per wave64 VALU: full-rate opcodes (v_add/v_xor/v_and/v_or/v_mov/"
+                                        "right shifts/bitop3) 2, paired in lock-step; rotates and every other VALU 4 "
+                                        "(profiles/r01_valu_issue_probes.md)",
            "kernels": kernels}
     dst = ROOT / "profiles" / f"isa_{src}.json"
     dst.write_text(json.dumps(res, indent=1) + "\n")
     print(dst)
     for k, v in kernels.items():
         if "wpr_kernel<false, true, 4u, false>" in k or "wpr_kernel<true, true, 4u, false>" in k:
-            print(k, {x: v[x] for x in ("arx_full", "arx_rot", "other_valu", "mfma", "clk_per_valu")})
+            print(k, {x: v[x] for x in ("arx_full", "arx_rot", "other_full", "other_half", "mfma", "clk_per_valu")})
 
 
 if __name__ == "__main__":

@@ -23,7 +23,7 @@ import sys
 from collections import Counter
 
 FULL = {"v_add_u32", "v_sub_u32", "v_xor_b32", "v_or_b32", "v_and_b32", "v_not_b32", "v_mov_b32",
-        "v_lshrrev_b32", "v_ashrrev_i32", "v_bitop3_b32", "v_subrev_u32"}
+        "v_lshrrev_b32", "v_ashrrev_i32", "v_bitop3_b32", "v_subrev_u32", "v_mov_b64"}
 
 
 def kernel_lines(path: str, name: str):
@@ -99,20 +99,33 @@ def census(body, blocks=False):
 
 
 def loop_body(lines):
-    """Lines of the outermost record loop: from the header label to the last
-    backward branch that targets a label before it."""
+    """Lines of the kernel's main loop: the smallest loop (a label and a
+    backward branch to it) that contains every ChaCha20 double-round asm block
+    -- the record loop of the wave-per-record kernel, the chunk-round loop of
+    the packed kernel; the whole kernel when no loop holds them all."""
     labels = {}
+    arx = []
+    start = None
     for i, l in enumerate(lines):
         m = re.match(r"^(\.LBB\S+):", l)
         if m:
             labels[m.group(1)] = i
+        s = l.strip()
+        if s.startswith(";;#ASMSTART"):
+            start = i
+        elif s.startswith(";;#ASMEND") and start is not None:
+            if any(x.strip().startswith("v_alignbit_b32") for x in lines[start:i]):
+                arx.append((start, i))
+            start = None
     best = None
     for i, l in enumerate(lines):
         m = re.match(r"^\s+s_(?:cbranch_\w+|branch)\s+(\.LBB\S+)", l)
         if m and m.group(1) in labels and labels[m.group(1)] < i:
-            span = i - labels[m.group(1)]
-            if best is None or span > best[1] - best[0]:
-                best = (labels[m.group(1)], i)
+            lo = labels[m.group(1)]
+            if arx and not all(lo <= a and b <= i for a, b in arx):
+                continue
+            if best is None or i - lo < best[1] - best[0]:
+                best = (lo, i)
     if best is None:
         return lines
     return lines[best[0]:best[1] + 1]

@@ -72,12 +72,19 @@ def main(tag: str, records: int = 1 << 20, record_bytes: int = 16384):
     # its keying dispatch.  For C1 a batch is exactly one aead kernel launch.
     acc = collections.defaultdict(lambda: collections.defaultdict(float))
     nbatch = collections.defaultdict(lambda: collections.defaultdict(int))
+    # SQ_INSTS_VALU per record kernel (by name) of the seal / open batches, for
+    # bench.py's per-kernel issue bound (valu_roofline of mixed batches)
+    valu_by = collections.defaultdict(lambda: collections.defaultdict(float))
+    valu_file = None
     for f in sorted(src.glob("pmc_*/run_counter_collection.csv")):
         seen = set()
         for r in csv.DictReader(open(f)):
             k = kind(r["Kernel_Name"])
             if not k:
                 continue
+            if k in ("seal", "open") and r["Counter_Name"] == "SQ_INSTS_VALU":
+                valu_by[k][r["Kernel_Name"]] += float(r["Counter_Value"])
+                valu_file = f.parent.name
             acc[k][r["Counter_Name"]] += float(r["Counter_Value"])
             nbatch[k][r["Counter_Name"]] += 0
             key = (k, r["Dispatch_Id"])
@@ -131,6 +138,9 @@ def main(tag: str, records: int = 1 << 20, record_bytes: int = 16384):
             traffic[f"{k}_clock_ghz"] = summ[k]["GRBM_GUI_ACTIVE"] / 8 / summ[k]["dispatch_ns"]
         if k in summ and "SQ_INSTS_VALU" in summ[k]:
             traffic[f"{k}_valu_per_record"] = summ[k]["SQ_INSTS_VALU"] / records
+        if valu_by.get(k) and valu_file:
+            nb = batches(k, valu_file)
+            traffic[f"{k}_valu_by_kernel"] = {name: v / nb for name, v in valu_by[k].items()}
     # the build string of the library the profiled bench ran (its JSON line in
     # the kernel-trace log), so a summary can never be stamped with a newer build
     log = src / "kt_bench.log"

@@ -124,8 +124,12 @@ def main():
         if p.returncode != 0:
             raise SystemExit(f"threads={t} failed:\n{p.stdout}\n{p.stderr}")
         runs[str(t)] = json.loads(p.stdout.strip().splitlines()[-1])
+    from suruga_amd import _native as N
+
+    lib = N.load()
     out = {"config": f"C4 host side: {a.bytes} B application data, {a.call_bytes} B per sg_write_records call, "
                      "pageable host buffers, one direction at a time, wall clock around the calls",
+           "kernels": lib.sg_build_info().decode(), "library": N.loaded_info(),
            "host_cpus": len(os.sched_getaffinity(0)), "by_copy_threads": runs,
            "correct": all(r["correct"] for r in runs.values())}
     print(json.dumps(out))

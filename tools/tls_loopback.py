@@ -228,6 +228,10 @@ def main():
 
         faulthandler.dump_traceback_later(args.watchdog, exit=True)
     out = run(args.bytes, args.write_chunk, args.device)
+    from suruga_amd import _native as N
+
+    out["kernels"] = N.load().sg_build_info().decode()
+    out["library"] = N.loaded_info()
     line = json.dumps(out)
     print(line)
     if args.json_out:
