@@ -20,3 +20,8 @@ for w in ("c1", "c2"):
     print(w, j["value"], "ms/step", j["ms_per_step"], "frac", j["roofline"]["frac"], "kernel_ms", j["kernel_ms"]["seal"],
           j["kernel_ms"]["open"], j["kernel_ms"]["keying"], "correct", j["correct"], "cpu", (j["cpu_baseline"] or {}).get("value"))
 PY
+# C4 host side and the loopback stream with the same build (round 4)
+timeout -k 10 600 python -u tools/record_path_bench.py --json-out "$OUT/record_path.json" > "$OUT/record_path.log" 2>&1 || echo "record_path failed"
+tail -c 400 "$OUT/record_path.log"; echo
+timeout -k 10 600 python -u tools/tls_loopback.py --json-out "$OUT/loopback.json" --watchdog 500 > "$OUT/loopback.log" 2>&1 || echo "loopback failed"
+tail -c 400 "$OUT/loopback.log"; echo

@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--no-check", action="store_true", help="timing experiments with wrong tags")
     a = ap.parse_args()
     os.environ["SURUGA_GPU_LIB"] = a.lib
+    os.environ.setdefault("SURUGA_ALLOW_VARIANT", "1")  # a -D build carries a variant marker (_build)
     import torch
 
     from suruga_amd import batch as B
