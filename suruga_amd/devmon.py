@@ -24,11 +24,14 @@ def _read(path):
         return None
 
 
-def card_dirs():
+DRM = "/sys/class/drm"
+
+
+def card_dirs(drm: str = DRM):
     """sysfs device directories of the amdgpu PCI functions (partition
     platform devices, amdgpu_xcp_*, carry no hwmon and are skipped)."""
     devs = []
-    for d in sorted(glob.glob("/sys/class/drm/card[0-9]*/device")):
+    for d in sorted(glob.glob(os.path.join(drm, "card[0-9]*", "device"))):
         real = os.path.realpath(d)
         if real not in devs and (_read(os.path.join(d, "vendor")) or "").strip() == "0x1002" \
                 and glob.glob(os.path.join(d, "hwmon", "hwmon*")):
@@ -36,11 +39,11 @@ def card_dirs():
     return devs
 
 
-def pick_card(pci_bus_id: str | None):
+def pick_card(pci_bus_id: str | None, drm: str = DRM):
     """(the card whose PCI address equals `pci_bus_id`, how it was chosen).
     A node has several cards, most of them another job's: without an exact
     match nothing is sampled unless exactly one card is visible."""
-    devs = card_dirs()
+    devs = card_dirs(drm)
     if pci_bus_id:
         want = pci_bus_id.lower()
         for d in devs:
@@ -55,13 +58,13 @@ class Sampler:
     """Samples sclk (MHz) and board power (W) of one card every `period` s
     between start() and stop()."""
 
-    def __init__(self, pci_bus_id: str | None = None, period: float = 0.005):
+    def __init__(self, pci_bus_id: str | None = None, period: float = 0.005, drm: str = DRM):
         self.period = period
         self.dev = None
         self.files = {}
         self.static = {}
         self.pci_bus_id = pci_bus_id
-        d0, self.how = pick_card(pci_bus_id)
+        d0, self.how = pick_card(pci_bus_id, drm)
         for d in ([d0] if d0 else []):
             self.dev = d
             for hw in sorted(glob.glob(os.path.join(d, "hwmon", "hwmon*"))):
