@@ -184,3 +184,27 @@ def test_bench_c2_two_ranks_scatter_gather(gpu):
     sg = j["scatter_gather"]
     assert j["correct"] and sg["verified"] and sg["split"] == "byte_balanced_ranges" and sg["records"] == 2048
     assert sg["ranges"][0][0] == 0 and sg["ranges"][-1][1] == 2048
+
+
+def test_issue_roofline_model():
+    """valu_roofline: the ARX stream at 2 / 4 clocks per
+    add-xor / rotate, the other VALU split by the census's full-rate share,
+    priced at the sampled clock; C2 prices each kernel's PMC VALU with its
+    census mix; missing inputs are reported, not guessed."""
+    sys.path.insert(0, str(ROOT))
+    import bench
+
+    name = "void sg::(anonymous namespace)::sg_wpr_kernel<false, true, 4u, false>(sg::KParams, sg::WprList)"
+    isa = {"model": "m", "kernels": {name: {"arx_full": 2448, "arx_rot": 1228, "other_valu": 672, "other_full": 336,
+                                            "valu": 4348, "clk_per_valu": 2.72, "clk_per_valu_whole": 2.72}}}
+    tj = {"seal_valu_per_record": 4320.0}
+    r = bench.issue_roofline("seal", "c1", 1 << 20, 256, 7.25, tj, isa, 1750.0)
+    clk = 2 * 2448 + 4 * 1228 + (4320 - 3676) * (2 * 0.5 + 4 * 0.5)
+    assert r["issue_clk_per_record"] == pytest.approx(clk, abs=0.1)
+    assert r["issue_bound_ms"] == pytest.approx(clk * 1024 / 1750e3, rel=1e-3)
+    assert r["frac"] == pytest.approx(r["issue_bound_ms"] / 7.25, rel=1e-3)
+    tj2 = {"seal_valu_by_kernel": {name: 1.0e9}}
+    r2 = bench.issue_roofline("seal", "c2", 1 << 20, 256, 1.3, tj2, isa, 2200.0)
+    assert r2["issue_bound_ms"] == pytest.approx(1.0e9 * 2.72 / 1024 / 2200e3, rel=1e-3)
+    assert "unavailable" in bench.issue_roofline("seal", "c1", 1 << 20, 256, 7.25, tj, None, 1750.0)
+    assert "unavailable" in bench.issue_roofline("seal", "c1", 1 << 20, 256, 7.25, tj, isa, None)
