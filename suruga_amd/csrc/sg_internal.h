@@ -116,17 +116,20 @@ constexpr uint32_t kWprN = 16384;
 //   [88 count, 248 count)           wave-per-record keying records (by slot)
 //   [248 count, 260 count)          wave-per-record descriptors (by slot)
 //   [260 count, 272 count)          kNumLists record lists
-//   then kNumLists populations, the over-long count, kWprBuckets + 1 group counters
+//   then kNumLists populations, the over-long count, kWprBuckets + 1 group
+//   counters and the packed launch's run counter
 constexpr uint32_t kWsWprTab = kKeyRecWords;
 constexpr uint32_t kWsWprDesc = kWsWprTab + kWprRecWords;
 constexpr uint32_t kWsLists = kWsWprDesc + kWprDescWords;
 constexpr uint32_t kWsRecWords = kWsLists + kNumLists;
-constexpr uint32_t kWsTailWords = kNumLists + 1u + kWprBuckets + 1u;
+constexpr uint32_t kWsTailWords = kNumLists + 1u + kWprBuckets + 2u;
 __host__ __device__ inline uint64_t ws_words(uint32_t count) { return (uint64_t)count * kWsRecWords + kWsTailWords; }
 // the counts / counters tail
 __host__ __device__ inline uint32_t* ws_tail(uint32_t* ws, uint32_t count) { return ws + (uint64_t)count * kWsRecWords; }
 constexpr uint32_t kTailOver = kNumLists;           // records longer than max_n
 constexpr uint32_t kTailCtr = kNumLists + 1u;       // + b: group counter of wpr bucket b, + kWprBuckets: uniform C1 launch
+constexpr uint32_t kTailPackCtr = kTailCtr + kWprBuckets + 1u;  // run counter of the packed launch
+hipError_t device_cus(int* cus);  // CUs of the current device (cached)
 
 // A wave-per-record bucket launch (mixed batch) or the uniform launch (list NULL).
 struct WprList {
@@ -160,11 +163,14 @@ const char* class_kernel_config();
 // Seal/open launch of a batch that is not a uniform 16 KiB one.  uniform:
 // every record is in size_class(max_n) (keying, direct launch); otherwise
 // classify into the workspace lists (kNumLists x count, populations in the
-// tail), key the listed records and launch per list: the wave-per-record
-// buckets (p.wpr_mix) first, then the size classes.  The tail's over-long count receives the records
-// longer than max_n, which are skipped (open: status 3); *over receives that
-// count when the populations are read back (not under capture).
+// tail), key the listed records and launch per list: the packed kernel
+// (p.pack_mix) ahead of the population readback, the wave-per-record buckets
+// (p.wpr_mix) and the size classes after it, on up to three streams that are
+// joined into s before the call returns.  The tail's over-long count receives
+// the records longer than max_n, which are skipped (open: status 3); *over
+// receives that count when the populations are read back (not under capture).
 // ev_keyed / ev_start (may be NULL) are recorded after the keying pre-passes
+// (mixed batches: after classify, before the packed launch)
 hipError_t launch_aead(const KParams& p, bool open, uint32_t max_n, bool uniform, hipStream_t s, uint32_t* over,
                        hipEvent_t ev_keyed, hipEvent_t ev_start);
 // Eligibility of one record of a mixed batch for the wave-per-record buckets:
@@ -179,7 +185,10 @@ __host__ __device__ inline bool pack_ok(uint32_t n, uint64_t in_addr, uint64_t o
 }
 bool pack_enabled();  // sg_set_packed / SG_PACK environment switch
 int set_pack(int enable);
-hipError_t launch_pack(const KParams& p, bool open, const uint32_t* list, uint32_t count, hipStream_t s);
+// packed launch on a persistent grid: the list's population *cnt and the run
+// counter *ctr (zero at launch) live on the device
+hipError_t launch_pack(const KParams& p, bool open, const uint32_t* list, const uint32_t* cnt, uint32_t* ctr,
+                       hipStream_t s);
 const char* pack_kernel_config();
 // zero the output of every record whose open status is 1 (wrong mac)
 hipError_t launch_scrub(const KParams& p, hipStream_t s);

@@ -780,24 +780,90 @@ hipError_t launch_class(uint32_t c, const KParams& q, const uint32_t* list, cons
 // as many buffers as calls were ever in flight at once; they live as long as
 // the process.
 std::mutex g_pop_mu;
-std::vector<uint32_t*> g_pop_free;
+std::vector<std::pair<uint32_t*, hipEvent_t>> g_pop_free;
 struct PinnedPop {
     uint32_t* p = nullptr;
+    hipEvent_t ev = nullptr;  // recorded after the readback copy
     hipError_t acquire(size_t bytes) {
         {
             std::lock_guard<std::mutex> lk(g_pop_mu);
             if (!g_pop_free.empty()) {
-                p = g_pop_free.back();
+                p = g_pop_free.back().first;
+                ev = g_pop_free.back().second;
                 g_pop_free.pop_back();
                 return hipSuccess;
             }
         }
-        return hipHostMalloc((void**)&p, bytes < 256u ? 256u : bytes, hipHostMallocDefault);
+        hipError_t e = hipHostMalloc((void**)&p, bytes < 256u ? 256u : bytes, hipHostMallocDefault);
+        if (e != hipSuccess) {
+            p = nullptr;
+            return e;
+        }
+        if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) {
+            (void)hipHostFree(p);
+            p = nullptr;
+            ev = nullptr;
+        }
+        return e;
     }
     ~PinnedPop() {
         if (!p) return;
         std::lock_guard<std::mutex> lk(g_pop_mu);
-        g_pop_free.push_back(p);
+        g_pop_free.emplace_back(p, ev);
+    }
+};
+
+// Side streams of mixed batches (per device, pooled like the pinned
+// population buffers, created non-blocking; they live as long as the process)
+std::mutex g_side_mu;
+std::vector<std::pair<int, std::pair<hipStream_t, hipEvent_t>>> g_side_free;
+struct SideStream {
+    hipStream_t s = nullptr;
+    hipEvent_t done = nullptr;
+    int dev = -1;
+    hipError_t acquire() {
+        hipError_t e = hipGetDevice(&dev);
+        if (e != hipSuccess) return e;
+        {
+            std::lock_guard<std::mutex> lk(g_side_mu);
+            for (size_t i = 0; i < g_side_free.size(); ++i)
+                if (g_side_free[i].first == dev) {
+                    s = g_side_free[i].second.first;
+                    done = g_side_free[i].second.second;
+                    g_side_free.erase(g_side_free.begin() + (long)i);
+                    return hipSuccess;
+                }
+        }
+        if ((e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking)) != hipSuccess) {
+            s = nullptr;
+            return e;
+        }
+        if ((e = hipEventCreateWithFlags(&done, hipEventDisableTiming)) != hipSuccess) {
+            (void)hipStreamDestroy(s);
+            s = nullptr;
+        }
+        return e;
+    }
+    // the batch's stream s waits for everything enqueued here so far
+    hipError_t join_into(hipStream_t t) const {
+        hipError_t e = hipEventRecord(done, s);
+        return e != hipSuccess ? e : hipStreamWaitEvent(t, done, 0);
+    }
+    ~SideStream() {
+        if (!s) return;
+        std::lock_guard<std::mutex> lk(g_side_mu);
+        g_side_free.push_back({dev, {s, done}});
+    }
+};
+// Every side stream a batch used is joined into its stream on every way out of
+// launch_aead_t (the workspace is released on that stream).
+struct SideJoin {
+    hipStream_t s;
+    const SideStream* side[2];
+    bool used[2];
+    ~SideJoin() {
+        for (int i = 0; i < 2; ++i)
+            if (used[i]) (void)side[i]->join_into(s);
     }
 };
 
@@ -817,32 +883,58 @@ hipError_t launch_aead_t(const KParams& p, uint32_t max_n, bool uniform, hipStre
     }
     uint32_t* const tail = ws_tail(p.ws, p.count);
     uint32_t* const lists = p.ws + (uint64_t)p.count * kWsLists;
-    // populations, over-long count and the bucket group counters (the keying
-    // kernel resets the latter again): one dword fill
+    // populations, over-long count and the group / run counters (the keying
+    // kernel resets the bucket ones again): one dword fill
     if ((e = hipMemsetD32Async((hipDeviceptr_t)tail, 0, kWsTailWords, s)) != hipSuccess) return e;
     const uint32_t per_wg = kClassifyThreads * kClassifyPerThread;
     hipLaunchKernelGGL(sg_classify_kernel<OPEN>, dim3((p.count + per_wg - 1u) / per_wg), dim3(kClassifyThreads), 0, s,
                        p, lists, tail, max_n);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    // Read the list populations back (one stream sync per mixed batch) so that
+    // Read the list populations back (one host wait per mixed batch) so that
     // the keying kernels run over exactly the listed records and every list
     // on an exact grid; under stream capture the host cannot wait, so every
     // record is keyed and the classes run on persistent grids instead (and the
-    // caller leaves p.wpr_mix off: the wave-per-record buckets need their
-    // populations).
+    // caller leaves p.wpr_mix and p.pack_mix off: the wave-per-record buckets
+    // need their populations).
     // (into a pinned buffer from a process-wide pool: a DMA, no staging copy;
     // the buffer goes back to the pool when this call is done with it)
     uint32_t pop[kNumLists + 1];
     hipStreamCaptureStatus cap_status = hipStreamCaptureStatusNone;
     if ((e = hipStreamIsCapturing(s, &cap_status)) != hipSuccess) return e;
     const bool exact = cap_status == hipStreamCaptureStatusNone;
+    // Mixed batches run on up to three streams (round 4): the packed launch
+    // (its population stays on the device) goes ahead of the host's wait for
+    // the readback, so the GPU does not idle while the host waits and
+    // launches; the keying launches run on a side stream ks beside the packed
+    // launch's tail; the J = 4 and J = 3 buckets follow the keying on ks and on
+    // a second side stream, and J = 2 and the size classes on s, so that each
+    // persistent bucket grid takes the CU slots that the launches before it
+    // free and their tails overlap instead of adding up.
+    SideStream side[2];
+    SideJoin join{s, {&side[0], &side[1]}, {false, false}};
+    hipStream_t ks = s;
     if (exact) {
         PinnedPop pin;
         if ((e = pin.acquire(sizeof pop)) != hipSuccess) return e;
-        if ((e = hipMemcpyAsync(pin.p, tail, sizeof pop, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
-        if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+        if ((e = hipMemcpyAsync(pin.p, tail, sizeof pop, hipMemcpyDeviceToHost, s)) != hipSuccess ||
+            (e = hipEventRecord(pin.ev, s)) != hipSuccess)
+            return e;
+        // the batch's record window starts with the packed launch
+        if ((e = mark(ev_keyed, s)) != hipSuccess || (e = mark(ev_start, s)) != hipSuccess) return e;
+        ev_keyed = ev_start = nullptr;
+        if (p.pack_mix && (e = launch_pack(p, OPEN, lists + (uint64_t)kPackList * p.count, tail + kPackList,
+                                           tail + kTailPackCtr, s)) != hipSuccess)
+            return e;
+        if ((e = hipEventSynchronize(pin.ev)) != hipSuccess) return e;
         for (uint32_t i = 0; i <= kNumLists; ++i) pop[i] = pin.p[i];
         *over = pop[kTailOver];
+        uint32_t nbuckets = 0;
+        for (uint32_t b = 0; b < kWprBuckets; ++b) nbuckets += pop[kNumClasses + b];
+        if (((p.pack_mix && pop[kPackList] != 0u) || (p.wpr_mix && nbuckets != 0u)) && side[0].acquire() == hipSuccess) {
+            ks = side[0].s;
+            join.used[0] = true;
+            if ((e = hipStreamWaitEvent(ks, pin.ev, 0)) != hipSuccess) return e;  // after classify
+        }
         // size-class keying over the class lists only
         KeyJobs jobs = {};
         uint32_t grid = 0;
@@ -854,7 +946,7 @@ hipError_t launch_aead_t(const KParams& p, uint32_t max_n, bool uniform, hipStre
             grid += (pop[c] + kKeyingThreads - 1u) / kKeyingThreads;
             ++jobs.njobs;
         }
-        if ((e = launch_keying(p, OPEN, jobs, grid, s)) != hipSuccess) return e;
+        if ((e = launch_keying(p, OPEN, jobs, grid, ks)) != hipSuccess) return e;
     } else if ((e = launch_keying_all(p, OPEN, s)) != hipSuccess) {
         return e;
     }
@@ -872,17 +964,22 @@ hipError_t launch_aead_t(const KParams& p, uint32_t max_n, bool uniform, hipStre
             wl[b].ctr = tail + kTailCtr + b;
             base += nb;
         }
-        if ((e = launch_wpr_keying_lists(p, OPEN, wl, s)) != hipSuccess) return e;
+        if ((e = launch_wpr_keying_lists(p, OPEN, wl, ks)) != hipSuccess) return e;
+    }
+    hipStream_t js[kWprBuckets] = {s, ks, ks};  // bucket b (J = 2 + b)
+    if (ks != s) {  // s (J = 2, classes) and the second side stream (J = 3) wait for the keying
+        if ((e = side[0].join_into(s)) != hipSuccess) return e;
+        if (p.wpr_mix && side[1].acquire() == hipSuccess) {
+            join.used[1] = true;
+            if ((e = hipStreamWaitEvent(side[1].s, side[0].done, 0)) != hipSuccess) return e;
+            js[1] = side[1].s;
+        }
     }
     if ((e = mark(ev_keyed, s)) != hipSuccess || (e = mark(ev_start, s)) != hipSuccess) return e;
     if (p.wpr_mix && exact) {  // most chunks first
         for (int b = (int)kWprBuckets - 1; b >= 0; --b)
-            if ((e = launch_wpr_list(p, OPEN, kWprMinJ + (uint32_t)b, wl[b], s)) != hipSuccess) return e;
+            if ((e = launch_wpr_list(p, OPEN, kWprMinJ + (uint32_t)b, wl[b], js[b])) != hipSuccess) return e;
     }
-    // packed small records (keyed inside their kernel)
-    if (p.pack_mix && exact &&
-        (e = launch_pack(p, OPEN, lists + (uint64_t)kPackList * p.count, pop[kPackList], s)) != hipSuccess)
-        return e;
     // one launch per populated class, largest records first
     KParams q = p;
     for (int c = (int)size_class(max_n); c >= 0; --c) {
@@ -892,7 +989,7 @@ hipError_t launch_aead_t(const KParams& p, uint32_t max_n, bool uniform, hipStre
                                     exact ? pop[c] : 0xffffffffu, s)) != hipSuccess)
             return e;
     }
-    return hipSuccess;
+    return hipSuccess;  // (join: s waits for the side streams)
 }
 
 hipError_t launch_aead(const KParams& p, bool open, uint32_t max_n, bool uniform, hipStream_t s, uint32_t* over,

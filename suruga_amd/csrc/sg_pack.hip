@@ -17,6 +17,10 @@
 // a SIMD then issue their full-rate add / xor back to back.  Lanes without a
 // block (a round with no chunk for the wave, the tail of the last chunk) run
 // the rounds with EXEC off, which saves power (the launch is power-capped).
+// The grid is persistent (three workgroups per CU) and takes runs from a
+// device counter until the list's population, read from the workspace, is
+// used up: the host launches it before it has read the populations back
+// (sg_kernels.hip, launch_aead_t), so the GPU runs it while the host waits.
 //
 //   setup (waves 0-1, one lane per record): keystream block 0 -> r, s
 //     (chacha20_poly1305.rs:50-52, poly1305.rs:197-203), the powers
@@ -132,6 +136,7 @@ struct PackLds {
     uint32_t base[kPackChunks];       // first-chunk histogram, then records starting before chunk c
     uint32_t wtot;                    // wave 0's blocks (setup scan)
     uint32_t nchunks, total;
+    uint32_t run;
 };
 static_assert(sizeof(PackLds) <= 65536, "static LDS");
 static_assert(3 * sizeof(PackLds) <= 160 * 1024, "three workgroups per CU");
@@ -205,16 +210,11 @@ __device__ unsigned long long g_pack_prof[kProfWgs][kProfStamps];
 #define SG_STAMP(w, k)
 #endif
 
+// One run: records first .. first + nrec - 1 of the packed list.
 template <bool OPEN>
-__global__ __launch_bounds__(kPackThreads) void sg_pack_kernel(const KParams p, const uint32_t* __restrict__ list,
-                                                               const uint32_t count) {
-    __shared__ PackLds L;
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = uniform(tid >> 6);
-    // XCD-aware run order (as the list kernels): workgroup b runs on XCD b % 8
-    const uint32_t ng = gridDim.x, x8 = blockIdx.x & 7u, q8 = ng >> 3, r8 = ng & 7u;
-    const uint32_t run = x8 * q8 + (x8 < r8 ? x8 : r8) + (blockIdx.x >> 3);
-    const uint32_t first = run * kPackRecs;
-    const uint32_t nrec = count - first < kPackRecs ? count - first : kPackRecs;
+__device__ __forceinline__ void pack_run(const KParams& p, const uint32_t* __restrict__ list, const uint32_t first,
+                                         const uint32_t nrec, PackLds& L, const uint32_t tid, const uint32_t lane,
+                                         const uint32_t wave) {
 
     SG_STAMP(0u, 0);
     for (uint32_t i = tid; i < kPackBlocks / 32u; i += kPackThreads) L.bits[i] = 0u;
@@ -457,16 +457,43 @@ __global__ __launch_bounds__(kPackThreads) void sg_pack_kernel(const KParams p, 
     SG_STAMP(0u, 5);
 }
 
+// Persistent grid (three workgroups per CU, the LDS bound): the packed list's
+// population is read from the workspace tail (the host does not need it, so
+// the launch goes ahead of the population readback) and the 128-record runs
+// come from a device counter, so that the runs' different lengths even out.
+template <bool OPEN>
+__global__ __launch_bounds__(kPackThreads) __attribute__((amdgpu_waves_per_eu(6)))
+void sg_pack_kernel(const KParams p, const uint32_t* __restrict__ list, const uint32_t* __restrict__ cnt, uint32_t* ctr) {
+    __shared__ PackLds L;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = uniform(tid >> 6);
+    const uint32_t count = __builtin_amdgcn_readfirstlane(*cnt);
+    const uint32_t nruns = (count + kPackRecs - 1u) / kPackRecs;
+    for (;;) {
+        if (tid == 0u) L.run = atomicAdd(ctr, 1u);
+        __syncthreads();
+        const uint32_t run = __builtin_amdgcn_readfirstlane(L.run);
+        if (run >= nruns) break;  // (workgroup-uniform)
+        const uint32_t first = run * kPackRecs;
+        pack_run<OPEN>(p, list, first, count - first < kPackRecs ? count - first : kPackRecs, L, tid, lane, wave);
+        __syncthreads();  // the finish read the slots that the next run's setup rewrites, and L.run
+    }
+}
+
 }  // namespace
 
-hipError_t launch_pack(const KParams& p, bool open, const uint32_t* list, uint32_t count, hipStream_t s) {
-    if (count == 0) return hipSuccess;
+hipError_t launch_pack(const KParams& p, bool open, const uint32_t* list, const uint32_t* count, uint32_t* ctr,
+                       hipStream_t s) {
+    if (p.count == 0) return hipSuccess;
     if (!p.tls) return hipErrorInvalidValue;  // the MAC geometry is the 13-byte TLS AD's
-    const uint32_t grid = (count + kPackRecs - 1u) / kPackRecs;
+    int cus = 0;
+    hipError_t e;
+    if ((e = device_cus(&cus)) != hipSuccess) return e;
+    const uint32_t most = (p.count + kPackRecs - 1u) / kPackRecs;
+    const uint32_t grid = 3u * (uint32_t)cus < most ? 3u * (uint32_t)cus : most;  // three workgroups per CU
     if (open)
-        hipLaunchKernelGGL((sg_pack_kernel<true>), dim3(grid), dim3(kPackThreads), 0, s, p, list, count);
+        hipLaunchKernelGGL((sg_pack_kernel<true>), dim3(grid), dim3(kPackThreads), 0, s, p, list, count, ctr);
     else
-        hipLaunchKernelGGL((sg_pack_kernel<false>), dim3(grid), dim3(kPackThreads), 0, s, p, list, count);
+        hipLaunchKernelGGL((sg_pack_kernel<false>), dim3(grid), dim3(kPackThreads), 0, s, p, list, count, ctr);
     return hipGetLastError();
 }
 
@@ -499,8 +526,9 @@ int set_pack(int enable) {
 }
 
 const char* pack_kernel_config() {
-    return "sg_pack_kernel v4: mixed-batch TLS records of 64 B-4 KiB (multiples of 64 B) packed 64-byte block per lane "
-           "across 128-record runs (512-thread workgroups, chunk rounds, lock-step grouped ChaCha20 rounds with EXEC limited "
+    return "sg_pack_kernel v5: mixed-batch TLS records of 64 B-4 KiB (multiples of 64 B) packed 64-byte block per lane "
+           "across 128-record runs (512-thread workgroups on a persistent grid taking runs from a device counter, launched "
+           "ahead of the population readback; chunk rounds, lock-step grouped ChaCha20 rounds with EXEC limited "
            "to the lanes holding a block; chunks to SIMD pairs first, waves without a chunk in the last round keep "
            "only the barriers), keying in the same kernel "
            "(block 0, r^(1+32a) and r^(4b) tables in LDS), per-lane Poly1305 share as a 4-step radix-2^32 Horner times "

@@ -1259,7 +1259,7 @@ extern "C" int sg_wpr_profile_read(unsigned long long* host, size_t n) {
 namespace sg {
 #endif
 
-static hipError_t device_cus(int* cus) {
+hipError_t device_cus(int* cus) {
     int dev = 0;
     hipError_t e;
     if ((e = hipGetDevice(&dev)) != hipSuccess) return e;

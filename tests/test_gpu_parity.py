@@ -718,17 +718,19 @@ def small_form(request, gpu):
     lib.sg_set_packed(prev)
 
 
-@pytest.mark.parametrize("count", [777, 9000])
-def test_mixed_batch_packed_small_records(gpu, oracle, small_form, count):
+@pytest.mark.parametrize("count,buckets", [(777, True), (9000, True), (2500, False)])
+def test_mixed_batch_packed_small_records(gpu, oracle, small_form, count, buckets):
     """Mixed TLS batches whose 64 B-4 KiB records (multiples of 64 bytes,
-    16-byte aligned) run on the packed kernel (sg_pack.hip: 64-record runs,
-    blocks end to end over the lanes, keyed in the kernel), beside records of
-    other lengths (size classes) and 4-16 KiB ones (wave-per-record buckets);
-    and the same batch on the size classes (small_form 0).  Every block count
-    1..64 occurs, runs of sixty-four 4 KiB records fill a run's 64 chunks, and
-    the count is not a multiple of the run size.  Every byte against the
-    oracle; open with tampering in the first byte, the last ciphertext byte and
-    the tag of packed records, and a truncated record."""
+    16-byte aligned) run on the packed kernel (sg_pack.hip: 128-record runs
+    from a device counter on a persistent grid, blocks end to end over the
+    lanes, keyed in the kernel), beside records of other lengths (size classes)
+    and 4-16 KiB ones (wave-per-record buckets; none with buckets=False, so
+    that only the packed launch and the classes run beside the keying
+    stream); and the same batch on the size classes (small_form 0).  Every
+    block count 1..64 occurs, runs of sixty-four 4 KiB records fill a run's 64
+    chunks, and the count is not a multiple of the run size.  Every byte
+    against the oracle; open with tampering in the first byte, the last
+    ciphertext byte and the tag of packed records, and a truncated record."""
     torch = torch_mod()
     from suruga_amd import batch as B
 
@@ -739,8 +741,8 @@ def test_mixed_batch_packed_small_records(gpu, oracle, small_form, count):
     lens[100:300] = 4096                       # whole runs of 64 x 64 blocks
     lens[300:364] = 64 * (np.arange(64) + 1)   # every block count
     odd = rng.random(count) < 0.1
-    lens[odd] = rng.integers(0, 4200, size=int(odd.sum())).astype(np.uint32)  # size classes
-    big = rng.random(count) < 0.03
+    lens[odd] = rng.integers(0, 4200 if buckets else 4096, size=int(odd.sum())).astype(np.uint32)  # size classes
+    big = rng.random(count) < (0.03 if buckets else 0.0)
     lens[big] = (64 * rng.integers(65, 257, size=int(big.sum()))).astype(np.uint32)  # buckets
     step_i = (lens.astype(np.uint64) + 15) // 16 * 16
     step_o = (lens.astype(np.uint64) + 16 + 15) // 16 * 16
