@@ -784,6 +784,7 @@ std::vector<std::pair<uint32_t*, hipEvent_t>> g_pop_free;
 struct PinnedPop {
     uint32_t* p = nullptr;
     hipEvent_t ev = nullptr;  // recorded after the readback copy
+    bool inflight = false;    // a copy into p may still be running
     hipError_t acquire(size_t bytes) {
         {
             std::lock_guard<std::mutex> lk(g_pop_mu);
@@ -808,6 +809,9 @@ struct PinnedPop {
     }
     ~PinnedPop() {
         if (!p) return;
+        // (an error return between the copy and the wait: the buffer goes back
+        // to the pool only once the copy into it is done)
+        if (inflight) (void)hipEventSynchronize(ev);
         std::lock_guard<std::mutex> lk(g_pop_mu);
         g_pop_free.emplace_back(p, ev);
     }
@@ -916,6 +920,7 @@ hipError_t launch_aead_t(const KParams& p, uint32_t max_n, bool uniform, hipStre
     if (exact) {
         PinnedPop pin;
         if ((e = pin.acquire(sizeof pop)) != hipSuccess) return e;
+        pin.inflight = true;
         if ((e = hipMemcpyAsync(pin.p, tail, sizeof pop, hipMemcpyDeviceToHost, s)) != hipSuccess ||
             (e = hipEventRecord(pin.ev, s)) != hipSuccess)
             return e;
@@ -926,6 +931,7 @@ hipError_t launch_aead_t(const KParams& p, uint32_t max_n, bool uniform, hipStre
                                            tail + kTailPackCtr, s)) != hipSuccess)
             return e;
         if ((e = hipEventSynchronize(pin.ev)) != hipSuccess) return e;
+        pin.inflight = false;
         for (uint32_t i = 0; i <= kNumLists; ++i) pop[i] = pin.p[i];
         *over = pop[kTailOver];
         uint32_t nbuckets = 0;
