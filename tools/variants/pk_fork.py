@@ -1,3 +1,4 @@
+# (edits against the sources before the merge commit 620e6f4, which made pk_fork3 the product)
 # pk_persist + the keying launches of a mixed batch on a side stream, beside
 # the packed launch: the bucket keying (latency-bound, ~2.8 waves per SIMD)
 # fills the packed launch's tail instead of running alone after it; the

@@ -1,3 +1,4 @@
+# (edits against the sources before the merge commit 620e6f4, which made pk_fork3 the product)
 # pk_fork + the three bucket launches on three streams (J = 2 on the batch's
 # stream, J = 3 on a second side stream, J = 4 after the keying on the keying
 # stream), all after the keying: each persistent bucket grid takes the CU

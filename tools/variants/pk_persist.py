@@ -1,3 +1,4 @@
+# (edits against the sources before the merge commit 620e6f4, which made pk_fork3 the product)
 # packed kernel on a persistent grid (three workgroups per CU) that reads its
 # population from the workspace tail and takes 128-record runs from a device
 # counter; launched right after the population readback is enqueued, so the

@@ -1,3 +1,4 @@
+# (edits against the sources before the merge commit 620e6f4, which made pk_fork3 the product)
 # pk_persist's persistent packed kernel, launched where the exact-grid one was
 # (after the population readback and the bucket launches): separates the cost
 # of the persistent loop from the gain of overlapping the readback wait
