@@ -838,6 +838,8 @@ def main():
     wpr_on = args.workload == "c1" and n == 16384 and lib.sg_set_lockstep(-1) == 1
     if args.workload == "c1":
         dom_kernel = f"sg_wpr_kernel<{dom.upper()}>" if wpr_on else f"sg_aead_kernel<{dom.upper()}, 256>"
+        if dom == "open":  # (the open window also holds the failed-record scrub: one status byte per record)
+            dom_kernel += " + sg_scrub_kernel"
     else:
         dom_kernel = (f"sg_wpr_kernel<{dom.upper()}, J=2..4> + sg_pack_kernel<{dom.upper()}> + size classes (one batch; "
                       "its classify and keying launches are timed apart, kernel_ms.keying)")
