@@ -163,7 +163,10 @@ typedef struct sg_batch {
      * than one size class) waits once for its classification so that every
      * class runs on an exact grid; under stream capture it does not wait
      * (persistent class grids), so the whole call is graph-capturable with a
-     * caller workspace.  NULL: the null (default) stream -- ordered after the
+     * caller workspace.  A mixed TLS batch also runs its keying and two of its
+     * record launches on library-owned side streams, which wait for this
+     * stream's earlier work and are joined back into it before the call
+     * returns.  NULL: the null (default) stream -- ordered after the
      * caller's earlier work on it -- and the call returns when the batch is
      * done.  No library lock is held while a call waits, so calls on
      * different streams (e.g. a writer and a reader thread, client.rs:19-24)
