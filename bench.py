@@ -66,6 +66,10 @@ def parse():
                     help="records per rank moved by the separately timed RCCL scatter/gather (N > 1; 0 = off)")
     ap.add_argument("--strong", action="store_true",
                     help="strong scaling: --records in total, split across ranks (default: weak, per rank)")
+    ap.add_argument("--c2-steps", type=int, default=60,
+                    help="C1 runs: timed steps of the C2 sub-record appended to the line (0 = none)")
+    ap.add_argument("--energy-seconds", type=float, default=2.0,
+                    help="length of the energy window after the event-timed steps (0 = no energy fields)")
     ap.add_argument("--traffic", default=None,
                     help="PMC-derived HBM traffic summary (tools/pmc_traffic.py)")
     return ap.parse_args()
@@ -608,6 +612,278 @@ def launch_ranks(args):
     return bad[0] if bad else 0
 
 
+def make_workload(args, workload, count, seq0, dev, stream):
+    """Device buffers and batch descriptors of one workload (C1: uniform 16 KiB
+    records, one key; C2: the Zipf layout with 256 connection keys), inputs
+    generated on the device."""
+    import numpy as np
+    import torch
+
+    from suruga_amd import batch as B
+
+    n = args.record_bytes
+    w = {"workload": workload, "count": count, "seq0": seq0, "n": n, "lay": None, "cs": None}
+    ws = torch.empty(B.workspace_size(count), dtype=torch.uint8, device=dev)
+    status = torch.empty(count, dtype=torch.uint8, device=dev)
+    if workload == "c1":
+        keys = torch.tensor(list(KEY), dtype=torch.uint8, device=dev).view(1, 32)
+        pt = torch.empty(count * n, dtype=torch.uint8, device=dev)
+        cs = args.ct_stride or (n + 16 + 127) // 128 * 128
+        if cs < n + 16 or cs % 16:
+            raise SystemExit("--ct-stride must be >= n + 16 and a multiple of 16")
+        ct = torch.empty(count * cs, dtype=torch.uint8, device=dev)
+        back = torch.empty(count * n, dtype=torch.uint8, device=dev)
+        B.fill_records(pt, n, n, count, SEED, j0=seq0)
+        seal_b = B.Batch(count=count, keys=keys, inp=pt, out=ct, uniform_len=n, in_stride=n, out_stride=cs,
+                         seq0=seq0, workspace=ws, stream=stream)
+        open_b = B.Batch(count=count, keys=keys, inp=ct, out=back, uniform_len=n + 16, in_stride=cs,
+                         out_stride=n, seq0=seq0, status=status, workspace=ws, stream=stream)
+        w["payload_per_step"] = 2 * count * n
+        w["alg"] = {"seal": (2 * n + 69) * count, "open": (2 * n + 70) * count}
+        w["alg_read"] = {"seal": (n + 53) * count, "open": (n + 69) * count}  # R alone: pt|ct(+tag) + ad + nonce + key
+        cfg = {"workload": f"C1: {count} x {n} B TLS records per GPU, one key, sequential seq, seal then open, "
+                           "device-resident", "records_per_gpu": count, "record_bytes": n}
+        cfg["layout"] = (f"plaintext records back to back ({n} B stride); sealed records (ct||tag) at a {cs} B "
+                         f"stride" + (" (128-byte aligned slots)" if cs % 128 == 0 and cs != n + 16 else ""))
+        w["cmp_args"] = (pt, n, back, n, n, count)
+        w["cs"] = cs
+    else:
+        from suruga_amd import workloads as W
+
+        lay = W.c2_layout(count, ct_align=args.c2_ct_align, pt_align=args.c2_pt_align)
+        t64 = lambda a: torch.from_numpy(a.view(np.int64)).to(dev)  # noqa: E731
+        t32 = lambda a: torch.from_numpy(a.view(np.int32)).to(dev)  # noqa: E731
+        keys = torch.tensor(list(lay.keys), dtype=torch.uint8, device=dev).view(-1, 32)
+        pt = torch.empty(lay.pt_bytes, dtype=torch.uint8, device=dev)
+        ct = torch.empty(lay.ct_bytes, dtype=torch.uint8, device=dev)
+        back = torch.empty(lay.pt_bytes, dtype=torch.uint8, device=dev)
+        B.fill_records(pt, 0, lay.pt_bytes, 1, SEED, j0=seq0)
+        if args.c2_pt_align != 64:  # padding between plaintext records: zero in pt and back (the compare is 64-byte granules)
+            starts = torch.from_numpy(lay.in_off.view(np.int64)).to(dev)
+            ln = torch.from_numpy(lay.lens.astype(np.int64)).to(dev)
+            mark = torch.zeros(lay.pt_bytes + 1, dtype=torch.int32, device=dev)
+            mark.index_add_(0, starts, torch.ones_like(starts, dtype=torch.int32))
+            mark.index_add_(0, starts + ln, -torch.ones_like(starts, dtype=torch.int32))
+            real = torch.cumsum(mark, 0)[:lay.pt_bytes] > 0
+            pt[~real] = 0
+            back.zero_()
+        lens, olens = t32(lay.lens), t32(lay.lens + 16)
+        in_off, out_off, kidx = t64(lay.in_off), t64(lay.out_off), t32(lay.key_index)
+        seqs = t64(lay.seq + np.uint64(seq0 // 256))
+        maxl = int(lay.lens.max())
+        seal_b = B.Batch(count=count, keys=keys, inp=pt, out=ct, lens=lens, max_len=maxl, in_off=in_off,
+                         out_off=out_off, key_index=kidx, seq=seqs, workspace=ws, stream=stream)
+        open_b = B.Batch(count=count, keys=keys, inp=ct, out=back, lens=olens, max_len=maxl + 16, in_off=out_off,
+                         out_off=in_off, key_index=kidx, seq=seqs, status=status, workspace=ws, stream=stream)
+        w["payload_per_step"] = 2 * lay.payload
+        w["alg"] = {"seal": 2 * lay.payload + 69 * count, "open": 2 * lay.payload + 70 * count}
+        w["alg_read"] = {"seal": lay.payload + 53 * count, "open": lay.payload + 69 * count}
+        cfg = {"workload": f"C2: {count} TLS records per GPU, Zipf(1.1) sizes 64 B-16 KiB (mean "
+                           f"{lay.payload / count:.0f} B), 256 connection keys, seal then open, device-resident",
+                           "records_per_gpu": count, "record_bytes": "zipf",
+                           "layout": (f"plaintext records {args.c2_pt_align}-byte aligned"
+                                      + (" (back to back)" if args.c2_pt_align == 64 else "")
+                                      + f"; sealed records {args.c2_ct_align}-byte aligned")}
+        w["cmp_args"] = (pt, 64, back, 64, 64, lay.pt_bytes // 64)  # 64-byte granules
+        w["lay"] = lay
+    w.update(keys=keys, pt=pt, ct=ct, back=back, ws=ws, status=status, seal_b=seal_b, open_b=open_b, cfg=cfg,
+             seal_c=seal_b.to_c(), open_c=open_b.to_c())
+    return w
+
+
+def energy_fields(mon_e, tm_e, count, dom):
+    """Energy per record at the power cap: the board power
+    averaged over the second half of a >= --energy-seconds window of event-timed
+    steps (power1_average is a running average that climbs from idle through a
+    short run, so the first half is dropped), times each launch's event time in
+    that same window, per record of the launch."""
+    pw = (mon_e.get("board_power_w") or {}).get("mean")
+    if not pw or not tm_e.get("seal_ms"):
+        return {"unavailable": "no board power reading" if not pw else "no event-timed launches"}
+    uj = lambda ms: round(pw * ms * 1e-3 / count * 1e6, 3)  # noqa: E731
+    return {"board_power_w": pw, "sclk_mhz": (mon_e.get("sclk_mhz") or {}).get("mean"),
+            "seal_ms": round(tm_e["seal_ms"], 4), "open_ms": round(tm_e["open_ms"], 4),
+            "keying_ms": round(tm_e["keying_ms"], 4),
+            "seal_uj_per_record": uj(tm_e["seal_ms"]), "open_uj_per_record": uj(tm_e["open_ms"]),
+            "keying_uj_per_record": uj(tm_e["keying_ms"]),
+            "energy_per_record_uj": uj(tm_e[f"{dom}_ms"]),
+            "window_s": round(mon_e.get("window_s", 0.0), 3), "launches": int(tm_e.get("n_seal", 0)),
+            "note": "board power (sysfs, mean of the window's second half) x event-timed launch time / records"}
+
+
+def run_measurement(args, w, steps, warmup, dist, backend, rank, local, local_dev, dev, stream, sampler, lib, bus):
+    """Warm-up, the timed region (barrier + sync on both sides, MAX over ranks),
+    event-timed kernel times right after it, an energy window, and the checks of
+    the last step (outside every timed region)."""
+    import ctypes as C
+
+    import torch
+
+    from suruga_amd import batch as B
+    from suruga_amd import shard
+
+    seal_c, open_c = w["seal_c"], w["open_c"]
+
+    def step():
+        B.N.check(lib.sg_seal_batch(C.byref(seal_c)))
+        B.N.check(lib.sg_open_batch(C.byref(open_c)))
+
+    torch.cuda.synchronize()  # inputs and tables made on the default stream
+    for _ in range(warmup):
+        step()
+    t_region0 = time.perf_counter()
+    elapsed = shard.timed(dist, step, steps, sync=torch.cuda.synchronize,
+                          device=dev if backend == "nccl" else None)
+    t_region1 = time.perf_counter()
+
+    # per-kernel device time with HIP events on the launch stream, right after
+    # the timed steps while the GPU is still at its steady-state clock (round 2
+    # took them after the CPU oracle fold, on a GPU that had idled for seconds)
+    B.set_timing(True)
+    t_ev0 = time.perf_counter()
+    for _ in range(max(5, min(steps, 10))):
+        step()
+    tm = B.timing_read()  # (waits for the last event)
+    t_ev1 = time.perf_counter()
+    B.set_timing(False)
+    # energy window (round 5): event-timed steps for >= --energy-seconds, the
+    # board at its sustained power; its second half prices energy per record
+    tm_e, mon_e = None, None
+    if args.energy_seconds > 0:
+        # steps per half window from the timed region's step time (the calls
+        # are asynchronous: a wall-clock loop would only fill the queue)
+        half = max(5, int(0.5 * args.energy_seconds / max(elapsed / steps, 1e-4)))
+        t_e0 = time.perf_counter()
+        for _ in range(half):  # first half: the board's running power average settles
+            step()
+        torch.cuda.synchronize()
+        B.set_timing(True)
+        t_h0 = time.perf_counter()
+        for _ in range(half):
+            step()
+        tm_e = B.timing_read()  # (waits for the last event)
+        t_h1 = time.perf_counter()
+        B.set_timing(False)
+        mon_e = sampler.summary(t_h0, t_h1)
+        mon_e["window_s"] = t_h1 - t_e0
+    mon = sampler.summary(t_region0, t_region1)
+    # the clock of the event-timed steps, whose launch times the issue bound
+    # prices (round 4: in a short run the clock still climbs through the timed
+    # region, so its mean undercuts the clock the event-timed launches ran at)
+    mon["event_steps_sclk_mhz"] = sampler.summary(t_ev0, t_ev1)["sclk_mhz"]
+
+    # correctness of the last step (outside the timed region): every record
+    # round-trips, and every tag and a sample of records equal the oracle's;
+    # the verdict is the AND over all ranks
+    mism = torch.zeros(1, dtype=torch.int64, device=dev)
+    B.compare_records(*w["cmp_args"], mism, stream=stream)
+    torch.cuda.synchronize()
+    bad_status = int((w["status"] != 0).sum().item())
+    roundtrip_ok = int(mism.item()) == 0 and bad_status == 0
+    exact = None
+    if not args.no_bitexact:
+        torch.cuda.synchronize()
+        exact = bitexact_check(w["ct"], w["n"], w["count"], w["seq0"], w["cs"]) if w["workload"] == "c1" else \
+            bitexact_check_c2(w["lay"], w["pt"], w["ct"], w["seq0"] // 256)
+    if os.environ.get("SG_BENCH_CORRUPT_RANK") == str(rank) and exact is not None:
+        exact["bitexact_fold"] = False  # test hook (tests/test_bench_contract.py): a rank whose check fails
+    mine = {"rank": rank, "local_rank": local, "device": local_dev, "pci_bus": bus, "roundtrip_ok": roundtrip_ok,
+            "bitexact_fold": exact["bitexact_fold"] if exact else None,
+            "bitexact_sample": exact["bitexact_sample"] if exact else None}
+    correct, ranks, flags = rank_verdict(dist, mine)
+    return {"elapsed": elapsed, "tm": tm, "mon": mon, "tm_e": tm_e, "mon_e": mon_e, "exact": exact,
+            "correct": correct, "ranks": ranks, "flags": flags}
+
+
+def kernel_fields(args, w, r, steps, world, dist, backend, dev, lib, props):
+    """value, the dominant launch's HBM roofline (PMC traffic of the same build
+    and layout), its VALU issue bound and the event-timed kernel times."""
+    count, n, tm, mon = w["count"], w["n"], r["tm"], r["mon"]
+    total_payload_per_step = w["payload_per_step"] * world if not args.strong else int(
+        sum_over_ranks(dist, w["payload_per_step"], dev if backend == "nccl" else None))
+    value = total_payload_per_step * steps / r["elapsed"] / 2**30
+    ms_per_step = r["elapsed"] / steps * 1e3
+    # dominant kernel's roofline (algorithmic bytes per launch, SURVEY.md 8d):
+    # seal R+W = 2n + 69 per record, open = 2n + 70
+    dom = "open" if tm["open_ms"] >= tm["seal_ms"] else "seal"
+    alg_bytes = w["alg"][dom]
+    dom_ms = tm[f"{dom}_ms"]
+    achieved = alg_bytes / (dom_ms * 1e-3) / 1e9
+    achieved_read = w["alg_read"][dom] / (dom_ms * 1e-3) / 1e9
+    # the event-timed kernels of one step against the wall-clock step
+    kernel_sum_ms = tm["seal_ms"] + tm["open_ms"] + 2 * tm["keying_ms"]
+    cfg = w["cfg"]
+    traffic, traffic_src, tj = None, None, None
+    # the PMC traffic summary of this exact kernel build and workload (the newest
+    # profiles/traffic_*.json whose build string and record shape match)
+    build = lib.sg_build_info().decode()
+    cands = [Path(args.traffic)] if args.traffic else sorted(
+        (ROOT / "profiles").glob("traffic_*.json"), key=lambda q: q.stat().st_mtime, reverse=True)
+    for q in cands:
+        try:
+            tq = json.loads(q.read_text())
+        except (ValueError, OSError):
+            continue
+        if tq.get("records") == count and tq.get("record_bytes") == cfg["record_bytes"] and \
+                tq.get("kernels") == build and tq.get("layout") == cfg.get("layout") and \
+                tq.get(f"{dom}_bytes_per_launch"):
+            tj = tq
+            traffic = tq.get(f"{dom}_bytes_per_launch")
+            traffic_src = (f"profiles/{q.name}: rocprofv3 PMC FETCH_SIZE x 2 + WRITE_SIZE of this kernel build "
+                           "and record layout in a separate profiling run (not this run)")
+            break
+    # the static ISA census of the loaded library's sources (tools/isa_census.py)
+    from suruga_amd import batch as B
+
+    provenance = B.N.loaded_info()
+    isa = None
+    isa_path = ROOT / "profiles" / f"isa_{provenance['source_hash']}.json"
+    if isa_path.exists():
+        try:
+            isa = json.loads(isa_path.read_text())
+        except ValueError:
+            isa = None
+    sclk = (mon.get("sclk_mhz") or {}).get("mean")
+    sclk_ev = (mon.get("event_steps_sclk_mhz") or {}).get("mean") or sclk
+    valu = issue_roofline(dom, w["workload"], count, props.multi_processor_count, dom_ms, tj, isa, sclk_ev)
+    if valu.get("sclk_mhz") is not None:
+        valu["sclk_window"] = "event-timed steps (the launches avg_launch_ms is taken from)"
+    wpr_on = w["workload"] == "c1" and n == 16384 and lib.sg_set_lockstep(-1) == 1
+    if w["workload"] == "c1":
+        dom_kernel = f"sg_wpr_kernel<{dom.upper()}>" if wpr_on else f"sg_aead_kernel<{dom.upper()}, 256>"
+        if dom == "open":  # (the open window also holds the failed-record scrub: one status byte per record)
+            dom_kernel += " + sg_scrub_kernel"
+        keying_note = "kernel_ms.keying: the sg_wpr_keying_kernel pre-pass, timed apart from the record launch"
+    else:
+        # the mixed batch's record window opens before the packed launch, so it
+        # also holds the keying launches (side stream, beside the packed tail)
+        dom_kernel = (f"sg_wpr_kernel<{dom.upper()}, J=2..4> + sg_pack_kernel<{dom.upper()}> + size classes + their "
+                      "keying launches (one batch, from the packed launch to the last list)")
+        keying_note = ("kernel_ms.keying: the tail memset, sg_classify_kernel and the population readback; the "
+                       "keying launches are inside the seal/open window")
+    energy = energy_fields(r["mon_e"], r["tm_e"], count, dom) if r["mon_e"] is not None else None
+    return {
+        "value": value, "ms_per_step": ms_per_step, "dom": dom, "build": build, "provenance": provenance,
+        "sclk": sclk,
+        "roofline": {"bound": "hbm", "kernel": dom_kernel,
+                     "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
+                     "alg_bytes_per_launch": alg_bytes, "avg_launch_ms": round(dom_ms, 4),
+                     # SURVEY.md 8(d)'s read-only variant (the north star's "HBM-read roofline")
+                     "hbm_read": {"achieved": round(achieved_read, 1), "frac": round(achieved_read / HBM_PEAK_GBS, 4),
+                                  "alg_read_bytes_per_launch": w["alg_read"][dom]}},
+        "valu_roofline": valu,
+        "kernel_ms": {"seal": round(tm["seal_ms"], 4), "open": round(tm["open_ms"], 4),
+                      "keying": round(tm["keying_ms"], 4), "sum_per_step": round(kernel_sum_ms, 4),
+                      "sum_vs_step": round(kernel_sum_ms / ms_per_step, 4),
+                      "launches": int(tm.get("n_seal", 0)) + int(tm.get("n_open", 0)),
+                      "note": "HIP events on the launch stream over steps run right after the timed region; "
+                              + keying_note},
+        "energy": energy,
+        "records_per_s": round((args.records if args.strong else count * world) * steps / r["elapsed"], 1),
+    }
+
+
 def main():
     args = parse()
     rc = launch_ranks(args)
@@ -650,232 +926,81 @@ def main():
     # the batch calls run asynchronously on a stream of their own: on the NULL
     # (default) stream every call would end with a device sync (suruga_gpu.h)
     stream = torch.cuda.Stream(dev)
-    ws = torch.empty(B.workspace_size(count), dtype=torch.uint8, device=dev)
-    status = torch.empty(count, dtype=torch.uint8, device=dev)
-    if args.workload == "c1":
-        keys = torch.tensor(list(KEY), dtype=torch.uint8, device=dev).view(1, 32)
-        pt = torch.empty(count * n, dtype=torch.uint8, device=dev)
-        cs = args.ct_stride or (n + 16 + 127) // 128 * 128
-        if cs < n + 16 or cs % 16:
-            raise SystemExit("--ct-stride must be >= n + 16 and a multiple of 16")
-        ct = torch.empty(count * cs, dtype=torch.uint8, device=dev)
-        back = torch.empty(count * n, dtype=torch.uint8, device=dev)
-        B.fill_records(pt, n, n, count, SEED, j0=seq0)
-        seal_b = B.Batch(count=count, keys=keys, inp=pt, out=ct, uniform_len=n, in_stride=n, out_stride=cs,
-                         seq0=seq0, workspace=ws, stream=stream)
-        open_b = B.Batch(count=count, keys=keys, inp=ct, out=back, uniform_len=n + 16, in_stride=cs,
-                         out_stride=n, seq0=seq0, status=status, workspace=ws, stream=stream)
-        payload_per_step = 2 * count * n
-        alg = {"seal": (2 * n + 69) * count, "open": (2 * n + 70) * count}
-        alg_read = {"seal": (n + 53) * count, "open": (n + 69) * count}  # R alone: pt|ct(+tag) + ad + nonce + key
-        cfg = {"workload": f"C1: {count} x {n} B TLS records per GPU, one key, sequential seq, seal then open, "
-                           "device-resident", "records_per_gpu": count, "record_bytes": n}
-        cfg["layout"] = (f"plaintext records back to back ({n} B stride); sealed records (ct||tag) at a {cs} B "
-                         f"stride" + (" (128-byte aligned slots)" if cs % 128 == 0 and cs != n + 16 else ""))
-        cmp_args = (pt, n, back, n, n, count)
-    else:
-        import numpy as np
-
-        from suruga_amd import workloads as W
-
-        lay = W.c2_layout(count, ct_align=args.c2_ct_align, pt_align=args.c2_pt_align)
-        t64 = lambda a: torch.from_numpy(a.view(np.int64)).to(dev)
-        t32 = lambda a: torch.from_numpy(a.view(np.int32)).to(dev)
-        keys = torch.tensor(list(lay.keys), dtype=torch.uint8, device=dev).view(-1, 32)
-        pt = torch.empty(lay.pt_bytes, dtype=torch.uint8, device=dev)
-        ct = torch.empty(lay.ct_bytes, dtype=torch.uint8, device=dev)
-        back = torch.empty(lay.pt_bytes, dtype=torch.uint8, device=dev)
-        B.fill_records(pt, 0, lay.pt_bytes, 1, SEED, j0=seq0)
-        if args.c2_pt_align != 64:  # padding between plaintext records: zero in pt and back (the compare is 64-byte granules)
-            real = torch.zeros(lay.pt_bytes, dtype=torch.bool, device=dev)
-            starts = torch.from_numpy(lay.in_off.view(np.int64)).to(dev)
-            ln = torch.from_numpy(lay.lens.astype(np.int64)).to(dev)
-            mark = torch.zeros(lay.pt_bytes + 1, dtype=torch.int32, device=dev)
-            mark.index_add_(0, starts, torch.ones_like(starts, dtype=torch.int32))
-            mark.index_add_(0, starts + ln, -torch.ones_like(starts, dtype=torch.int32))
-            real = torch.cumsum(mark, 0)[:lay.pt_bytes] > 0
-            pt[~real] = 0
-            back.zero_()
-        lens, olens = t32(lay.lens), t32(lay.lens + 16)
-        in_off, out_off, kidx = t64(lay.in_off), t64(lay.out_off), t32(lay.key_index)
-        seqs = t64(lay.seq + np.uint64(seq0 // 256))
-        maxl = int(lay.lens.max())
-        seal_b = B.Batch(count=count, keys=keys, inp=pt, out=ct, lens=lens, max_len=maxl, in_off=in_off,
-                         out_off=out_off, key_index=kidx, seq=seqs, workspace=ws, stream=stream)
-        open_b = B.Batch(count=count, keys=keys, inp=ct, out=back, lens=olens, max_len=maxl + 16, in_off=out_off,
-                         out_off=in_off, key_index=kidx, seq=seqs, status=status, workspace=ws, stream=stream)
-        payload_per_step = 2 * lay.payload
-        alg = {"seal": 2 * lay.payload + 69 * count, "open": 2 * lay.payload + 70 * count}
-        alg_read = {"seal": lay.payload + 53 * count, "open": lay.payload + 69 * count}
-        cfg = {"workload": f"C2: {count} TLS records per GPU, Zipf(1.1) sizes 64 B-16 KiB (mean "
-                           f"{lay.payload / count:.0f} B), 256 connection keys, seal then open, device-resident",
-                           "records_per_gpu": count, "record_bytes": "zipf",
-                           "layout": (f"plaintext records {args.c2_pt_align}-byte aligned"
-                                      + (" (back to back)" if args.c2_pt_align == 64 else "")
-                                      + f"; sealed records {args.c2_ct_align}-byte aligned")}
-        cmp_args = (pt, 64, back, 64, 64, lay.pt_bytes // 64)  # 64-byte granules
-    seal_c, open_c = seal_b.to_c(), open_b.to_c()
+    w = make_workload(args, args.workload, count, seq0, dev, stream)
     lib = B.N.load()
-    import ctypes as C
-
-    def step():
-        B.N.check(lib.sg_seal_batch(C.byref(seal_c)))
-        B.N.check(lib.sg_open_batch(C.byref(open_c)))
-
-    torch.cuda.synchronize()  # inputs and tables made on the default stream
     # the shader clock and board power (sysfs, plain reads on a background
-    # thread from the warm-up to the end of the event-timed steps below): the
-    # issue-bound roofline is priced at the mean clock of the timed region
+    # thread from the warm-up to the end of the last measurement): the
+    # issue-bound roofline is priced at the mean clock of the event-timed steps
     from suruga_amd import devmon
 
     props = torch.cuda.get_device_properties(dev)
     bus = f"{props.pci_domain_id:04x}:{props.pci_bus_id:02x}:{props.pci_device_id:02x}.0"
     sampler = devmon.Sampler(bus).start()
-    for _ in range(args.warmup):
-        step()
-    t_region0 = time.perf_counter()
-    elapsed = shard.timed(dist, step, args.steps, sync=torch.cuda.synchronize,
-                          device=dev if backend == "nccl" else None)
-    t_region1 = time.perf_counter()
-
-    # per-kernel device time with HIP events on the launch stream, right after
-    # the timed steps while the GPU is still at its steady-state clock (round 2
-    # took them after the CPU oracle fold, on a GPU that had idled for seconds)
-    B.set_timing(True)
-    t_ev0 = time.perf_counter()
-    for _ in range(max(5, min(args.steps, 10))):
-        step()
-    tm = B.timing_read()  # (waits for the last event)
-    t_ev1 = time.perf_counter()
-    B.set_timing(False)
-    mon = sampler.stop(t_region0, t_region1)
-    # the clock of the event-timed steps, whose launch times the issue bound
-    # prices (round 4: in a short run the clock still climbs through the timed
-    # region, so its mean undercuts the clock the event-timed launches ran at)
-    mon["event_steps_sclk_mhz"] = sampler.summary(t_ev0, t_ev1)["sclk_mhz"]
-
-    # correctness of the last step (outside the timed region): every record
-    # round-trips, and every tag and a sample of records equal the oracle's;
-    # the verdict is the AND over all ranks
-    mism = torch.zeros(1, dtype=torch.int64, device=dev)
-    B.compare_records(*cmp_args, mism, stream=stream)
-    torch.cuda.synchronize()
-    bad_status = int((status != 0).sum().item())
-    roundtrip_ok = int(mism.item()) == 0 and bad_status == 0
-    exact = None
-    if not args.no_bitexact:
-        torch.cuda.synchronize()
-        exact = bitexact_check(ct, n, count, seq0, cs) if args.workload == "c1" else \
-            bitexact_check_c2(lay, pt, ct, seq0 // 256)
-    if os.environ.get("SG_BENCH_CORRUPT_RANK") == str(rank) and exact is not None:
-        exact["bitexact_fold"] = False  # test hook (tests/test_bench_contract.py): a rank whose check fails
-    mine = {"rank": rank, "local_rank": local, "device": local_dev, "pci_bus": bus, "roundtrip_ok": roundtrip_ok,
-            "bitexact_fold": exact["bitexact_fold"] if exact else None,
-            "bitexact_sample": exact["bitexact_sample"] if exact else None}
-    correct, ranks, flags = rank_verdict(dist, mine)
+    r = run_measurement(args, w, args.steps, args.warmup, dist, backend, rank, local, local_dev, dev, stream,
+                        sampler, lib, bus)
+    kf = kernel_fields(args, w, r, args.steps, world, dist, backend, dev, lib, props)
+    correct, ranks, flags, exact = r["correct"], r["ranks"], r["flags"], r["exact"]
 
     scatter_gather = None
     if world > 1 and args.sg_records > 0:
         try:  # a side measurement: a failure here is reported, not fatal to the device-resident line
             if args.workload == "c1":
-                scatter_gather = measure_scatter_gather(args, dist, backend, rank, world, dev, n, count, seq0, seal_b,
-                                                        lib, keys, ws, stream)
+                scatter_gather = measure_scatter_gather(args, dist, backend, rank, world, dev, n, count, seq0,
+                                                        w["seal_b"], lib, w["keys"], w["ws"], stream)
             else:
-                scatter_gather = measure_scatter_gather_c2(args, dist, backend, rank, world, dev, lay, keys, stream)
+                scatter_gather = measure_scatter_gather_c2(args, dist, backend, rank, world, dev, w["lay"], w["keys"],
+                                                           stream)
         except (RuntimeError, ValueError) as e:
             scatter_gather = {"error": f"{type(e).__name__}: {e}"[:300]}
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args, n) if args.workload == "c1" else cpu_baseline(args, 0, w["lay"])
 
-    # seal + open plaintext bytes of all ranks (weak: every rank the same count)
-    total_payload_per_step = payload_per_step * world if not args.strong else int(
-        sum_over_ranks(dist, payload_per_step, dev if backend == "nccl" else None))
-    payload = total_payload_per_step * args.steps
-    value = payload / elapsed / 2**30
-    ms_per_step = elapsed / args.steps * 1e3
-
-    # dominant kernel's roofline (algorithmic bytes per launch):
-    # seal R+W = 2n + 69 per record, open = 2n + 70
-    dom = "open" if tm["open_ms"] >= tm["seal_ms"] else "seal"
-    alg_bytes = alg[dom]
-    dom_ms = tm[f"{dom}_ms"]
-    achieved = alg_bytes / (dom_ms * 1e-3) / 1e9
-    achieved_read = alg_read[dom] / (dom_ms * 1e-3) / 1e9
-    # the event-timed kernels of one step against the wall-clock step
-    kernel_sum_ms = tm["seal_ms"] + tm["open_ms"] + 2 * tm["keying_ms"]
-    traffic, traffic_src, tj = None, None, None
-    # the PMC traffic summary of this exact kernel build and workload (the newest
-    # profiles/traffic_*.json whose build string and record shape match)
-    build = lib.sg_build_info().decode()
-    cands = [Path(args.traffic)] if args.traffic else sorted(
-        (ROOT / "profiles").glob("traffic_*.json"), key=lambda q: q.stat().st_mtime, reverse=True)
-    for q in cands:
-        try:
-            tq = json.loads(q.read_text())
-        except (ValueError, OSError):
-            continue
-        if tq.get("records") == count and tq.get("record_bytes") == cfg["record_bytes"] and \
-                tq.get("kernels") == build and tq.get("layout") == cfg.get("layout") and \
-                tq.get(f"{dom}_bytes_per_launch"):
-            tj = tq
-            traffic = tq.get(f"{dom}_bytes_per_launch")
-            traffic_src = (f"profiles/{q.name}: rocprofv3 PMC FETCH_SIZE x 2 + WRITE_SIZE of this kernel build "
-                           "and record layout in a separate profiling run (not this run)")
-            break
-    # the static ISA census of the loaded library's sources (tools/isa_census.py)
-    provenance = B.N.loaded_info()
-    isa = None
-    isa_path = ROOT / "profiles" / f"isa_{provenance['source_hash']}.json"
-    if isa_path.exists():
-        try:
-            isa = json.loads(isa_path.read_text())
-        except ValueError:
-            isa = None
-    sclk = (mon.get("sclk_mhz") or {}).get("mean")
-    sclk_ev = (mon.get("event_steps_sclk_mhz") or {}).get("mean") or sclk
-    valu = issue_roofline(dom, args.workload, count, props.multi_processor_count, dom_ms, tj, isa, sclk_ev)
-    if valu.get("sclk_mhz") is not None:
-        valu["sclk_window"] = "event-timed steps (the launches avg_launch_ms is taken from)"
-
-    wpr_on = args.workload == "c1" and n == 16384 and lib.sg_set_lockstep(-1) == 1
-    if args.workload == "c1":
-        dom_kernel = f"sg_wpr_kernel<{dom.upper()}>" if wpr_on else f"sg_aead_kernel<{dom.upper()}, 256>"
-        if dom == "open":  # (the open window also holds the failed-record scrub: one status byte per record)
-            dom_kernel += " + sg_scrub_kernel"
-    else:
-        dom_kernel = (f"sg_wpr_kernel<{dom.upper()}, J=2..4> + sg_pack_kernel<{dom.upper()}> + size classes (one batch; "
-                      "its classify and keying launches are timed apart, kernel_ms.keying)")
+    # the C2 sub-record: after the C1 line's measurement,
+    # the full Zipf batch of BASELINE.json configs[2] under the same protocol;
+    # `value` stays C1's.  Its correctness joins the line's.
+    c2 = None
+    cfg1 = w["cfg"]
+    if args.workload == "c1" and args.c2_steps > 0:
+        del w
+        torch.cuda.empty_cache()
+        w2 = make_workload(args, "c2", count, seq0, dev, stream)
+        r2 = run_measurement(args, w2, args.c2_steps, args.warmup, dist, backend, rank, local, local_dev, dev,
+                             stream, sampler, lib, bus)
+        k2 = kernel_fields(args, w2, r2, args.c2_steps, world, dist, backend, dev, lib, props)
+        c2 = {"metric": "GiB/s device-resident ChaCha20-Poly1305 over Zipf 64 B-16 KiB TLS records (C2)",
+              "value": round(k2["value"], 3), "unit": "GiB/s", "steps": args.c2_steps, "warmup": args.warmup,
+              "ms_per_step": round(k2["ms_per_step"], 4), "config": w2["cfg"], "roofline": k2["roofline"],
+              "valu_roofline": k2["valu_roofline"], "kernel_ms": k2["kernel_ms"], "energy": k2["energy"],
+              "sclk_mhz": k2["sclk"], "records_per_s": k2["records_per_s"], "correct": r2["correct"],
+              "ranks": r2["ranks"], **{kk: vv for kk, vv in (r2["exact"] or {}).items()},
+              **{kk: vv for kk, vv in r2["flags"].items() if vv is not None}}
+        correct = correct and r2["correct"]
+    sampler.stop()
     if rank == 0:
-        cpu = None
-        if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(args, n) if args.workload == "c1" else cpu_baseline(args, 0, lay)
         line = {
-            "metric": METRIC, "value": round(value, 3), "unit": "GiB/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
+            "metric": METRIC, "value": round(kf["value"], 3), "unit": "GiB/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(kf["ms_per_step"], 4),
             "higher_is_better": True, "scaling": "strong" if args.strong else "weak", "vs_baseline": None, "dtype": "u32",
             "data": "synthetic (splitmix64 records generated on device)",
-            "config": dict(cfg, parallelism=f"record-shard x{world}", kernels=build,
-                           library=provenance),
-            "roofline": {"bound": "hbm", "kernel": dom_kernel,
-                         "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
-                         "alg_bytes_per_launch": alg_bytes, "avg_launch_ms": round(dom_ms, 4),
-                         # SURVEY.md 8(d)'s read-only variant (the north star's "HBM-read roofline")
-                         "hbm_read": {"achieved": round(achieved_read, 1), "frac": round(achieved_read / HBM_PEAK_GBS, 4),
-                                      "alg_read_bytes_per_launch": alg_read[dom]}},
-            "valu_roofline": valu,
-            "sclk_mhz": sclk,
-            "board_power_w": (mon.get("board_power_w") or {}).get("last"),
-            "device_monitor": mon,
-            "kernel_ms": {"seal": round(tm["seal_ms"], 4), "open": round(tm["open_ms"], 4),
-                          "keying": round(tm["keying_ms"], 4), "sum_per_step": round(kernel_sum_ms, 4),
-                          "sum_vs_step": round(kernel_sum_ms / ms_per_step, 4),
-                          "launches": int(tm.get("n_seal", 0)) + int(tm.get("n_open", 0)),
-                          "note": "HIP events on the launch stream over steps run right after the timed region"},
-            "records_per_s": round((args.records if args.strong else count * world) * args.steps / elapsed, 1),
+            "config": dict(cfg1, parallelism=f"record-shard x{world}", kernels=kf["build"], library=kf["provenance"]),
+            "roofline": kf["roofline"],
+            "valu_roofline": kf["valu_roofline"],
+            "sclk_mhz": kf["sclk"],
+            "board_power_w": (r["mon"].get("board_power_w") or {}).get("last"),
+            "energy_per_record_uj": (kf["energy"] or {}).get("energy_per_record_uj"),
+            "energy": kf["energy"],
+            "device_monitor": r["mon"],
+            "kernel_ms": kf["kernel_ms"],
+            "records_per_s": kf["records_per_s"],
             "cpu_baseline": cpu,
         }
-        line.update(correctness_fields(correct, ranks, flags, exact))
+        line.update(correctness_fields(r["correct"], ranks, flags, exact))
+        line["correct"] = correct
         if scatter_gather is not None:
             line["scatter_gather"] = scatter_gather
+        if c2 is not None:
+            line["c2"] = c2
         print(json.dumps(line), flush=True)
     if dist:
         dist.barrier()

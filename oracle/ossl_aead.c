@@ -45,12 +45,31 @@ typedef struct {
 } tl_methods;
 static __thread tl_methods tl_m;
 
+/* The thread's contexts are freed when the thread exits (pthread key
+ * destructor): the pool threads live as long as the process, but every other
+ * thread that calls in (thread 0 of a batch is the caller) would otherwise
+ * leak one library context. */
+static pthread_key_t tl_key;
+static pthread_once_t tl_key_once = PTHREAD_ONCE_INIT;
+static void tl_free(void* v) {
+    tl_methods* m = (tl_methods*)v;
+    EVP_CIPHER_free(m->cipher);
+    EVP_MAC_free(m->mac);
+    OSSL_LIB_CTX_free(m->lib);
+    m->cipher = NULL;
+    m->mac = NULL;
+    m->lib = NULL;
+}
+static void tl_key_make(void) { (void)pthread_key_create(&tl_key, tl_free); }
+
 static int tl_fetch(void) {
     if (tl_m.lib == NULL) {
+        pthread_once(&tl_key_once, tl_key_make);
         tl_m.lib = OSSL_LIB_CTX_new();
         if (tl_m.lib == NULL) return 0;
         tl_m.cipher = EVP_CIPHER_fetch(tl_m.lib, "ChaCha20", NULL);
         tl_m.mac = EVP_MAC_fetch(tl_m.lib, "POLY1305", NULL);
+        (void)pthread_setspecific(tl_key, &tl_m);
     }
     return tl_m.cipher != NULL && tl_m.mac != NULL;
 }

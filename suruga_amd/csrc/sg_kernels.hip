@@ -783,8 +783,9 @@ std::mutex g_pop_mu;
 std::vector<std::pair<uint32_t*, hipEvent_t>> g_pop_free;
 struct PinnedPop {
     uint32_t* p = nullptr;
-    hipEvent_t ev = nullptr;  // recorded after the readback copy
-    bool inflight = false;    // a copy into p may still be running
+    hipEvent_t ev = nullptr;          // recorded after the readback copy
+    hipStream_t copy_s = nullptr;     // set once a copy into p has been enqueued on it
+    bool recorded = false;            // ev was recorded after that copy
     hipError_t acquire(size_t bytes) {
         {
             std::lock_guard<std::mutex> lk(g_pop_mu);
@@ -807,38 +808,60 @@ struct PinnedPop {
         }
         return e;
     }
+    void done() { copy_s = nullptr; }  // the copy has been waited for
     ~PinnedPop() {
         if (!p) return;
-        // (an error return between the copy and the wait: the buffer goes back
-        // to the pool only once the copy into it is done)
-        if (inflight) (void)hipEventSynchronize(ev);
+        // An error return between the copy and the wait: the buffer goes back to
+        // the pool only once the copy into it is known to be done -- by its event
+        // when that was recorded, else by the copy's stream.  If neither wait
+        // succeeds the buffer is dropped (leaked) rather than handed to another
+        // call while a DMA may still write it.
+        if (copy_s) {
+            const hipError_t w = recorded ? hipEventSynchronize(ev) : hipStreamSynchronize(copy_s);
+            if (w != hipSuccess) return;
+        }
         std::lock_guard<std::mutex> lk(g_pop_mu);
         g_pop_free.emplace_back(p, ev);
     }
 };
 
-// Side streams of mixed batches (per device, pooled like the pinned
-// population buffers, created non-blocking; they live as long as the process)
+// Side streams of mixed batches (per device and priority, pooled like the
+// pinned population buffers, created non-blocking with the priority of the
+// batch's stream; they live as long as the process).  A pooled stream is
+// handed out again only when its last join event reports done, i.e. every
+// kernel an earlier batch enqueued on it has finished: the SideStream goes
+// back to the pool when launch_aead_t returns, while its keying and bucket
+// kernels may still be queued, and a concurrent batch on another caller
+// stream must not queue behind them (calls on different streams are
+// independent, suruga_gpu.h).  A busy pooled stream is skipped and a new one
+// created.
 std::mutex g_side_mu;
-std::vector<std::pair<int, std::pair<hipStream_t, hipEvent_t>>> g_side_free;
+struct SidePooled {
+    int dev, prio;
+    hipStream_t s;
+    hipEvent_t done;
+};
+std::vector<SidePooled> g_side_free;
 struct SideStream {
     hipStream_t s = nullptr;
     hipEvent_t done = nullptr;
-    int dev = -1;
-    hipError_t acquire() {
+    int dev = -1, prio = 0;
+    hipError_t acquire(hipStream_t caller) {
         hipError_t e = hipGetDevice(&dev);
         if (e != hipSuccess) return e;
+        if ((e = hipStreamGetPriority(caller, &prio)) != hipSuccess) return e;
         {
             std::lock_guard<std::mutex> lk(g_side_mu);
-            for (size_t i = 0; i < g_side_free.size(); ++i)
-                if (g_side_free[i].first == dev) {
-                    s = g_side_free[i].second.first;
-                    done = g_side_free[i].second.second;
-                    g_side_free.erase(g_side_free.begin() + (long)i);
-                    return hipSuccess;
-                }
+            for (size_t i = 0; i < g_side_free.size(); ++i) {
+                const SidePooled& c = g_side_free[i];
+                if (c.dev != dev || c.prio != prio || hipEventQuery(c.done) != hipSuccess) continue;
+                s = c.s;
+                done = c.done;
+                g_side_free.erase(g_side_free.begin() + (long)i);
+                return hipSuccess;
+            }
         }
-        if ((e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking)) != hipSuccess) {
+        if ((e = hipStreamCreateWithPriority(&s, hipStreamNonBlocking, prio)) != hipSuccess) {
             s = nullptr;
             return e;
         }
@@ -856,7 +879,7 @@ struct SideStream {
     ~SideStream() {
         if (!s) return;
         std::lock_guard<std::mutex> lk(g_side_mu);
-        g_side_free.push_back({dev, {s, done}});
+        g_side_free.push_back({dev, prio, s, done});
     }
 };
 // Every side stream a batch used is joined into its stream on every way out of
@@ -920,10 +943,10 @@ hipError_t launch_aead_t(const KParams& p, uint32_t max_n, bool uniform, hipStre
     if (exact) {
         PinnedPop pin;
         if ((e = pin.acquire(sizeof pop)) != hipSuccess) return e;
-        pin.inflight = true;
-        if ((e = hipMemcpyAsync(pin.p, tail, sizeof pop, hipMemcpyDeviceToHost, s)) != hipSuccess ||
-            (e = hipEventRecord(pin.ev, s)) != hipSuccess)
-            return e;
+        if ((e = hipMemcpyAsync(pin.p, tail, sizeof pop, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+        pin.copy_s = s;
+        if ((e = hipEventRecord(pin.ev, s)) != hipSuccess) return e;
+        pin.recorded = true;
         // the batch's record window starts with the packed launch
         if ((e = mark(ev_keyed, s)) != hipSuccess || (e = mark(ev_start, s)) != hipSuccess) return e;
         ev_keyed = ev_start = nullptr;
@@ -931,12 +954,12 @@ hipError_t launch_aead_t(const KParams& p, uint32_t max_n, bool uniform, hipStre
                                            tail + kTailPackCtr, s)) != hipSuccess)
             return e;
         if ((e = hipEventSynchronize(pin.ev)) != hipSuccess) return e;
-        pin.inflight = false;
+        pin.done();
         for (uint32_t i = 0; i <= kNumLists; ++i) pop[i] = pin.p[i];
         *over = pop[kTailOver];
         uint32_t nbuckets = 0;
         for (uint32_t b = 0; b < kWprBuckets; ++b) nbuckets += pop[kNumClasses + b];
-        if (((p.pack_mix && pop[kPackList] != 0u) || (p.wpr_mix && nbuckets != 0u)) && side[0].acquire() == hipSuccess) {
+        if (((p.pack_mix && pop[kPackList] != 0u) || (p.wpr_mix && nbuckets != 0u)) && side[0].acquire(s) == hipSuccess) {
             ks = side[0].s;
             join.used[0] = true;
             if ((e = hipStreamWaitEvent(ks, pin.ev, 0)) != hipSuccess) return e;  // after classify
@@ -975,7 +998,7 @@ hipError_t launch_aead_t(const KParams& p, uint32_t max_n, bool uniform, hipStre
     hipStream_t js[kWprBuckets] = {s, ks, ks};  // bucket b (J = 2 + b)
     if (ks != s) {  // s (J = 2, classes) and the second side stream (J = 3) wait for the keying
         if ((e = side[0].join_into(s)) != hipSuccess) return e;
-        if (p.wpr_mix && side[1].acquire() == hipSuccess) {
+        if (p.wpr_mix && side[1].acquire(s) == hipSuccess) {
             join.used[1] = true;
             if ((e = hipStreamWaitEvent(side[1].s, side[0].done, 0)) != hipSuccess) return e;
             js[1] = side[1].s;

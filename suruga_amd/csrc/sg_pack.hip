@@ -442,9 +442,11 @@ __device__ __forceinline__ void pack_run(const KParams& p, const uint32_t* __res
         const uint32_t* sl = L.slot + m0 * kSlotWords;
         const uint32_t n = 64u * sl[kSNb], rec = sl[kSRec];
         const uint32_t* ac = L.acc + kAccWords * m0;
-        // (ACC64: v1 = lo + hi 2^32 -> hi 2^58 = (hi << 6) 2^52 joins limb 2)
-        F26 f = SG_PACK_ACC64 ? carry1(F26{ac[0], ac[4], ac[1] + (ac[5] << 6), ac[2], ac[3]})
+        // (ACC64: v1 = lo + hi 2^32 -> hi 2^58 = (hi << 6) 2^52 joins limb 2 after
+        // the first carry pass: limb 2's raw sum can reach 2^32 - 64, and hi <= 1)
+        F26 f = SG_PACK_ACC64 ? carry1(F26{ac[0], ac[4], ac[1], ac[2], ac[3]})
                               : carry1(F26{ac[0], ac[1], ac[2], ac[3], ac[4]});
+        if constexpr (SG_PACK_ACC64) f.v2 += ac[5] << 6;
         f = carry1(f26_add(f, load_f26(sl + kSCtot)));
         const uint32_t s[4] = {sl[kSS + 0], sl[kSS + 1], sl[kSS + 2], sl[kSS + 3]};
         uint32_t tw[4];

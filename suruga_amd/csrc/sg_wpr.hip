@@ -614,9 +614,16 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     // T fragment byte a' comes from the V window for a' < 16 - sigma, else from P
     const uint32_t nv = 16u - sigma;
     const u32x4 vmask = {~bytes_from(0u, nv), ~bytes_from(1u, nv), ~bytes_from(2u, nv), ~bytes_from(3u, nv)};
-    // LDS swizzle: 16-byte unit 4 t + c of a chunk lives at 4 t + (c ^ ((t >> 2) & 3))
-    const uint32_t wunit = (lane & ~3u) | ((lane ^ (lane >> 4)) & 3u);  // unit of global position 64 k + lane
-    const uint32_t xq = (lane >> 2) & 3u;
+    // LDS swizzle: 16-byte unit 4 t + c of a chunk lives at 4 t + (c ^ f(t)),
+    // f(t) = (t ^ (t >> 2)) & 3.  Conflict-free for all three
+    // accesses under the gfx950 banking rules (tests/test_lds_swizzle.py): the
+    // lanes' ds_read_b128 of their own block (16-lane groups, 64 banks), the
+    // staging ds_write_b128 (8 contiguous lanes, 32 banks: f is a bijection of
+    // t's bits 1-2 for each t bit 0) and the lane-contiguous read-out.  (Round 4's f = (t >> 2) & 3
+    // put lanes 8m and 8m + 2 of every write group on one bank slot: 8 conflict
+    // cycles per write, 128 per record, SQ_LDS_BANK_CONFLICT = 2^27 per launch.)
+    const uint32_t wunit = (lane & ~3u) | ((lane ^ (lane >> 2) ^ (lane >> 4)) & 3u);  // unit of global position 64 k + lane
+    const uint32_t xq = (lane ^ (lane >> 2)) & 3u;
     // the lane's MAC window base (line 5 (1 - hh), dword of byte 47 - q) and shift
     const uint8_t* mac_base = lines + 240u * (1u - hh) + 4u * ((47u - q) >> 2);
     const uint32_t mac_shift = (47u - q) & 3u;
@@ -686,7 +693,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     // previous chunk does not occupy, one chunk ahead: lane l of DMA piece k
     // lands at LDS unit 64 k + l and reads global unit 64 k + wunit(l), so LDS
     // unit phi(g) holds global unit g (phi = wunit within each 64-unit piece,
-    // an involution).  The record sits right-aligned in the 16 KiB frame:
+    // an involution: f depends only on the lane bits wunit keeps).  The record sits right-aligned in the 16 KiB frame:
     // frame byte v is record byte v - vs (vs = 2^14 - n), so the first chunk
     // j0 of a shorter record starts with lo = 4096 J - n bytes that belong to
     // no record; their lanes neither load nor store.  The record's keying
@@ -1223,10 +1230,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     if (pend) {  // the last record's last chunk
         wave_lds_sync();
         const uint8_t* pb = buf + kWprChunk * lastb;
+        // the lane index recomputed here (mbcnt) rather than kept live across the
+        // record loop: at 128 VGPRs a value held from the prologue to this tail
+        // is what the allocator spills first
+        const uint32_t ln = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
 #pragma unroll
         for (uint32_t k = 0; k < 4u; ++k)
-            if (!LIST || 1024u * k + 16u * lane >= pend_lo)
-                gst16(pend_dst + 1024u * k + 16u * lane, ld16(pb + 1024u * k + 16u * wunit));
+            if (!LIST || 1024u * k + 16u * ln >= pend_lo)
+                gst16(pend_dst + 1024u * k + 16u * ln, ld16(pb + 1024u * k + 16u * wunit));
     }
 #if SG_WPR_PROFILE
     SG_TICK(t_end);

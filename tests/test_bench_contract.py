@@ -43,6 +43,16 @@ def test_bench_single_gpu_small(gpu):
     j = _last_json(p.stdout)
     assert KEYS <= set(j) and j["n_gpus"] == 1 and j["correct"] and j["value"] > 0
     assert set(j["roofline"]) >= {"bound", "achieved", "peak", "unit", "frac", "traffic"}
+    # the C2 sub-record (BASELINE configs[2]) under the same protocol, checked against the oracle
+    c2 = j["c2"]
+    assert c2["correct"] and c2["bitexact_fold"] and c2["bitexact_sample"] and c2["value"] > 0
+    assert c2["steps"] == 60 and set(c2["roofline"]) >= {"achieved", "frac", "traffic"}
+    assert c2["config"]["record_bytes"] == "zipf" and c2["config"]["records_per_gpu"] == 4096
+    # energy per record over the energy window (board power x event-timed launch time / records)
+    e = j["energy"]
+    if "unavailable" not in e:
+        assert j["energy_per_record_uj"] == e["energy_per_record_uj"] > 0
+        assert e["board_power_w"] > 0 and e["seal_uj_per_record"] > 0 and e["open_uj_per_record"] > 0
 
 
 @pytest.mark.gpu
@@ -184,6 +194,42 @@ def test_bench_c2_two_ranks_scatter_gather(gpu):
     sg = j["scatter_gather"]
     assert j["correct"] and sg["verified"] and sg["split"] == "byte_balanced_ranges" and sg["records"] == 2048
     assert sg["ranges"][0][0] == 0 and sg["ranges"][-1][1] == 2048
+
+
+@pytest.mark.gpu
+def test_bench_two_real_devices(gpu):
+    """with two or more GPUs visible, `bench.py --gpus 2`
+    runs its ranks on two different cards (distinct PCI addresses) over RCCL
+    and the line is correct.  Skipped on a one-GPU box."""
+    import torch
+
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs two visible GPUs")
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT",
+                                                            "SG_DIST_BACKEND")}
+    p = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--records", "4096", "--steps", "2",
+                        "--warmup", "1", "--no-cpu-baseline", "--c2-steps", "0", "--energy-seconds", "0"],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    j = _last_json(p.stdout)
+    assert j["n_gpus"] == 2 and j["correct"]
+    assert [r["device"] for r in j["ranks"]] == [0, 1]
+    assert len({r["pci_bus"] for r in j["ranks"]}) == 2
+
+
+def test_energy_fields():
+    """energy_per_record_uj = mean board power of the window's second half x
+    the dominant launch's event time / records; reported as unavailable without
+    a power reading."""
+    sys.path.insert(0, str(ROOT))
+    import bench
+
+    tm = {"seal_ms": 7.2, "open_ms": 7.3, "keying_ms": 0.13, "n_seal": 100}
+    mon = {"board_power_w": {"mean": 1400.0}, "sclk_mhz": {"mean": 1850.0}, "window_s": 2.0}
+    e = bench.energy_fields(mon, tm, 1 << 20, "open")
+    assert e["energy_per_record_uj"] == pytest.approx(1400.0 * 7.3e-3 / (1 << 20) * 1e6, rel=1e-3)
+    assert e["seal_uj_per_record"] == pytest.approx(1400.0 * 7.2e-3 / (1 << 20) * 1e6, rel=1e-3)
+    assert "unavailable" in bench.energy_fields({"board_power_w": None}, tm, 1 << 20, "open")
 
 
 def test_issue_roofline_model():

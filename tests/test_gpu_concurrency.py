@@ -153,3 +153,100 @@ def test_device_batches_on_two_streams(gpu, oracle):
     assert bytes(ct.cpu().numpy().tobytes()) == ct_ref
     assert int((status != 0).sum().item()) == 0
     assert torch.equal(back, pt)
+
+
+def _mixed_layout(rng, count):
+    """A mixed TLS batch: packed 64 B-4 KiB records, 4-16 KiB bucket records
+    and ragged size-class records, 16-byte aligned slots."""
+    lens = (64 * rng.integers(1, 65, size=count)).astype(np.uint32)
+    big = rng.random(count) < 0.06
+    lens[big] = (64 * rng.integers(65, 257, size=int(big.sum()))).astype(np.uint32)
+    odd = rng.random(count) < 0.08
+    lens[odd] = rng.integers(0, 5000, size=int(odd.sum())).astype(np.uint32)
+    step_i = (lens.astype(np.uint64) + 15) // 16 * 16
+    step_o = (lens.astype(np.uint64) + 16 + 15) // 16 * 16
+    in_off = np.zeros(count, dtype=np.uint64)
+    out_off = np.zeros(count, dtype=np.uint64)
+    in_off[1:] = np.cumsum(step_i[:-1])
+    out_off[1:] = np.cumsum(step_o[:-1])
+    return lens, in_off, out_off, int(in_off[-1] + step_i[-1]), int(out_off[-1] + step_o[-1])
+
+
+def test_mixed_batches_on_two_streams(gpu, oracle):
+    """mixed batches fork onto pooled side streams; two
+    threads run mixed TLS batches (packed, bucket and size-class records) on
+    two caller streams of different priority, many times over, so that the side
+    streams one call returns to the pool are asked for by the other call while
+    its kernels may still be queued.  A side stream is reused only once idle,
+    so the batches stay independent; every byte against the oracle."""
+    import struct
+
+    import torch
+
+    from suruga_amd import batch as B
+
+    N, lib = _lib()
+    rng = np.random.default_rng(5)
+    dev = torch.device("cuda", 0)
+    lo, hi = torch.cuda.Stream.priority_range() if hasattr(torch.cuda.Stream, "priority_range") else (0, -1)
+    sa, sb = torch.cuda.Stream(dev), torch.cuda.Stream(dev, priority=min(lo, hi))
+    tdev = lambda a: torch.from_numpy(a.view(np.int64) if a.dtype == np.uint64 else a.view(np.int32)).to(dev)  # noqa: E731
+    jobs = []
+    for j, st in enumerate((sa, sb)):
+        count = 1500 + 300 * j
+        lens, in_off, out_off, pt_bytes, ct_bytes = _mixed_layout(rng, count)
+        keys_h = rng.bytes(16 * 32)
+        kidx = rng.integers(0, 16, size=count).astype(np.uint32)
+        seqs = rng.integers(0, 2**40, size=count, dtype=np.uint64)
+        pt_h = rng.bytes(pt_bytes)
+        exp = bytearray(ct_bytes)
+        for i in range(count):
+            k = keys_h[32 * int(kidx[i]):32 * int(kidx[i]) + 32]
+            s, n, o, q = int(seqs[i]), int(lens[i]), int(in_off[i]), int(out_off[i])
+            exp[q:q + n + 16] = oracle.seal(k, struct.pack(">Q", s), pt_h[o:o + n], oracle.tls_ad(s, n))
+        keys = torch.frombuffer(bytearray(keys_h), dtype=torch.uint8).to(dev).view(16, 32)
+        ws = torch.empty(B.workspace_size(count), dtype=torch.uint8, device=dev)
+        common = dict(count=count, keys=keys, key_index=tdev(kidx), seq=tdev(seqs), workspace=ws, stream=st)
+        if j == 0:  # thread A seals
+            out = torch.zeros(ct_bytes, dtype=torch.uint8, device=dev)
+            b = B.Batch(inp=torch.frombuffer(bytearray(pt_h), dtype=torch.uint8).to(dev), out=out, lens=tdev(lens),
+                        max_len=int(lens.max()), in_off=tdev(in_off), out_off=tdev(out_off), **common)
+            jobs.append((lib.sg_seal_batch, b, out, bytes(exp), None, None))
+        else:       # thread B opens
+            out = torch.zeros(pt_bytes, dtype=torch.uint8, device=dev)
+            status = torch.full((count,), 0xFF, dtype=torch.uint8, device=dev)
+            olens = (lens + 16).astype(np.uint32)
+            b = B.Batch(inp=torch.frombuffer(bytearray(exp), dtype=torch.uint8).to(dev), out=out, lens=tdev(olens),
+                        max_len=int(olens.max()), in_off=tdev(out_off), out_off=tdev(in_off), status=status, **common)
+            want = bytearray(pt_bytes)
+            for i in range(count):
+                o, n = int(in_off[i]), int(lens[i])
+                want[o:o + n] = pt_h[o:o + n]
+            jobs.append((lib.sg_open_batch, b, out, bytes(want), status, (lens, in_off)))
+    torch.cuda.synchronize()
+    cs = [job[1].to_c() for job in jobs]
+    errs = []
+
+    def run(fn, c):
+        try:
+            for _ in range(12):
+                N.check(fn(C.byref(c)))
+        except Exception as e:  # reported below
+            errs.append(repr(e))
+
+    th = [threading.Thread(target=run, args=(job[0], c)) for job, c in zip(jobs, cs)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    torch.cuda.synchronize()
+    assert not errs, errs
+    fn, b, out, want, status, meta = jobs[0]
+    got = out.cpu().numpy().tobytes()
+    assert got == want, "seal thread's batch differs from the oracle"
+    fn, b, out, want, status, (lens, in_off) = jobs[1]
+    assert int((status != 0).sum().item()) == 0
+    got = out.cpu().numpy().tobytes()
+    for i in range(len(lens)):
+        o, n = int(in_off[i]), int(lens[i])
+        assert got[o:o + n] == want[o:o + n], i
