@@ -243,6 +243,22 @@ int sg_read_records(sg_ctx* ctx, uint64_t seq0, const uint8_t* wire, size_t wire
                     size_t out_cap, uint8_t* types, uint32_t* frag_lens, size_t max_records,
                     sg_read_result* res);
 
+/* The header checks of sg_read_records alone (TlsReader::read_record,
+ * tls.rs:217-238, 258-262, 269-272), host only -- no context, no GPU: the
+ * complete records at the start of `wire` (at most max_records) go to `recs`
+ * (offset of the fragment after its 5-byte header, fragment length, type,
+ * version), *count of them; *error = SG_OK, or the error of the first bad
+ * header (SG_E_UNEXPECTED_MESSAGE, SG_E_RECORD_OVERFLOW, SG_E_SHORT) that
+ * stopped the parse.  An incomplete record at the end is not an error.
+ * Returns SG_OK or SG_E_ARG. */
+typedef struct sg_wire_record {
+    uint64_t offset;
+    uint32_t frag_len;
+    uint8_t  type, ver_major, ver_minor, _pad;
+} sg_wire_record;
+int sg_parse_records(const uint8_t* wire, size_t wire_len, size_t max_records, sg_wire_record* recs,
+                     size_t* count, int32_t* error);
+
 /* Time (ms) spent by the last sg_write_records / sg_read_records call of this
  * thread in host->device copies, kernels and device->host copies (HIP events;
  * summed over the pipelined chunks) and in host-side framing memcpy. */

@@ -154,23 +154,32 @@ so_int1305 so_int1305_mult(so_int1305 a, so_int1305 b) {
 #undef M
 #undef M5
     uint64_t carry = 0;
+/* debug_assert_eq!(v[i] >> 32, 0) for every limb (poly1305.rs:87-91, 103-107, 119-123) */
+#define LIMBS_FIT_32()                                                              \
+    do {                                                                            \
+        for (int i_ = 0; i_ < 5; ++i_) SO_DEBUG_ASSERT((v[i_] >> 32) == 0);         \
+    } while (0)
 #define REDUCE_DIGIT(i)           \
     do {                          \
         v[i] += carry;            \
         carry = v[i] >> 26;       \
         v[i] &= (1ull << 26) - 1; \
     } while (0)
-    /* pass 1 :81-85 */
+    /* pass 1 :81-85, then the limb and carry bounds of :87-93 */
     REDUCE_DIGIT(0); REDUCE_DIGIT(1); REDUCE_DIGIT(2); REDUCE_DIGIT(3); REDUCE_DIGIT(4);
+    LIMBS_FIT_32();
     SO_DEBUG_ASSERT(carry <= 25ull * ((1ull << 26) - 1));
     carry *= 5; /* :95 */
-    /* pass 2 :97-101 */
+    /* pass 2 :97-101, bounds :103-109 */
     REDUCE_DIGIT(0); REDUCE_DIGIT(1); REDUCE_DIGIT(2); REDUCE_DIGIT(3); REDUCE_DIGIT(4);
+    LIMBS_FIT_32();
     SO_DEBUG_ASSERT(carry <= 1);
     carry *= 5; /* :111 */
-    /* pass 3 :113-117 */
+    /* pass 3 :113-117, bounds :119-125 */
     REDUCE_DIGIT(0); REDUCE_DIGIT(1); REDUCE_DIGIT(2); REDUCE_DIGIT(3); REDUCE_DIGIT(4);
+    LIMBS_FIT_32();
     SO_DEBUG_ASSERT(carry == 0);
+#undef LIMBS_FIT_32
 #undef REDUCE_DIGIT
     so_int1305 r = {{(uint32_t)v[0], (uint32_t)v[1], (uint32_t)v[2], (uint32_t)v[3],
                      (uint32_t)v[4]}};

@@ -24,8 +24,9 @@ ORACLE_DIR = ROOT / "oracle"
 ORACLE_LIB = ORACLE_DIR / "liboracle.so"
 
 HIP_SOURCES = [CSRC / "sg_kernels.hip", CSRC / "sg_wpr.hip", CSRC / "sg_pack.hip", CSRC / "sg_capi.cpp", CSRC / "sg_record.cpp",
-               CSRC / "sg_keysched.cpp"]
-HIP_DEPS = HIP_SOURCES + [CSRC / "sg_internal.h", CSRC / "sg_device.h", CSRC / "sg_host.h", CSRC / "sg_chacha_grp.inc",
+               CSRC / "sg_keysched.cpp", CSRC / "sg_wire.cpp"]
+HIP_DEPS = HIP_SOURCES + [CSRC / "sg_internal.h", CSRC / "sg_device.h", CSRC / "sg_host.h", CSRC / "sg_err.h",
+                          CSRC / "sg_wire.h", CSRC / "sg_chacha_grp.inc",
                           ROOT / "include" / "suruga_gpu.h"]
 ORACLE_SOURCES = [ORACLE_DIR / "suruga_oracle.c"]
 ORACLE_DEPS = ORACLE_SOURCES + [ORACLE_DIR / "suruga_oracle.h", ORACLE_DIR / "so_pool.h"]

@@ -7,11 +7,10 @@
 #include <mutex>
 
 #include "../../include/suruga_gpu.h"
+#include "sg_err.h"
 
 namespace sg {
 
-// thread-local last-error message (sg_last_error)
-int fail(int code, const char* fmt, const char* detail = nullptr);
 int hip_fail(hipError_t e, const char* where);
 
 struct RecordStaging;                   // sg_record.cpp

@@ -12,7 +12,7 @@
 #include <vector>
 
 #include "../../include/suruga_gpu.h"
-#include "sg_host.h"
+#include "sg_err.h"  // host only: no HIP (tests/cpp/test_host_san.cpp builds it with g++ under sanitizers)
 
 namespace sg {
 namespace {

@@ -23,6 +23,7 @@
 
 #include "../../include/suruga_gpu.h"
 #include "sg_host.h"
+#include "sg_wire.h"
 #include "sg_internal.h"
 
 namespace sg {
@@ -370,37 +371,10 @@ int sg_read_records(sg_ctx* c, uint64_t seq0, const uint8_t* wire, size_t wire_l
     t_h2d = t_kernel = t_d2h = t_host = 0;
 
     // 1. parse complete records (tls.rs:218-238), stopping at the first bad header
-    struct Rec {
-        size_t off;      // wire offset of the fragment
-        uint32_t flen;   // fragment length (ct || tag)
-        uint8_t type, major, minor;
-    };
+    // (sg_wire.cpp: host-only, run under ASan/UBSan by tests/test_sanitizers.py)
+    using Rec = WireRec;
     std::vector<Rec> recs;
-    size_t pos = 0;
-    int32_t header_error = SG_OK;
-    while (pos + SG_HEADER_LEN <= wire_len && recs.size() < max_records) {
-        const uint8_t* h = wire + pos;
-        if (h[0] < 20 || h[0] > 23) {  // ContentType 20..23 (tls.rs:19-29, 218-225)
-            header_error = SG_E_UNEXPECTED_MESSAGE;
-            break;
-        }
-        const uint32_t flen = ((uint32_t)h[3] << 8) | h[4];
-        if (flen > SG_ENC_RECORD_MAX_LEN) {  // tls.rs:232-234
-            header_error = SG_E_RECORD_OVERFLOW;
-            break;
-        }
-        if (pos + SG_HEADER_LEN + flen > wire_len) break;  // incomplete: wait for more bytes
-        if (flen < SG_MAC_LEN) {  // tls.rs:258-262 "encrypted message too short"
-            header_error = SG_E_SHORT;
-            break;
-        }
-        if (flen - SG_MAC_LEN > SG_RECORD_MAX_LEN) {  // tls.rs:269-272 (reference panics)
-            header_error = SG_E_RECORD_OVERFLOW;
-            break;
-        }
-        recs.push_back({pos + SG_HEADER_LEN, flen, h[0], h[1], h[2]});
-        pos += SG_HEADER_LEN + flen;
-    }
+    const int32_t header_error = parse_wire(wire, wire_len, max_records, recs);
     size_t need = 0;
     for (const Rec& r : recs) need += r.flen - SG_MAC_LEN;
     if (need > out_cap || (need && !out)) return fail(SG_E_ARG, "out buffer too small%s");

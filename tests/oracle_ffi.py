@@ -7,6 +7,7 @@ bench.py's cpu_baseline leg load it.
 from __future__ import annotations
 
 import ctypes as C
+import os
 import sys
 from pathlib import Path
 
@@ -33,6 +34,9 @@ class Int1305(C.Structure):
 
 class Oracle:
     def __init__(self, path: Path | None = None):
+        if path is None and os.environ.get("SURUGA_ORACLE_LIB"):
+            # another build of the same restatement (tests/test_sanitizers.py: -DSO_DEBUG, ASan/UBSan)
+            path = Path(os.environ["SURUGA_ORACLE_LIB"])
         if path is None:
             from suruga_amd._build import build_oracle
 
