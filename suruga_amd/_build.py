@@ -84,7 +84,7 @@ FORBIDDEN_DEFINE_PREFIXES = ("-DSG_LS_NO", "-DSG_LS_COMPILED", "-DSG_EXP_", "-DS
 
 def build_library(force: bool = False, out: Path | None = None, defines=()) -> Path:
     """Compile the gfx950 HIP library (seconds).  ``out``/``defines`` build an
-    experiment variant (e.g. ``-DSG_SALU_PRE=0``) next to the product library;
+    experiment variant (e.g. ``-DSG_WPR_PROFILE=1``) next to the product library;
     the product library itself is only ever built without defines."""
     target = Path(out) if out else LIB
     bad = [d for d in defines if str(d).startswith(FORBIDDEN_DEFINE_PREFIXES)]

@@ -34,7 +34,7 @@ EXPORTS = [
     "sg_workspace_size", "sg_seal_batch", "sg_open_batch",
     "sg_fill_records", "sg_compare_records",
     "sg_last_error", "sg_build_info", "sg_source_hash", "sg_set_timing", "sg_timing_read", "sg_set_lockstep", "sg_set_packed",
-    "sg_wire_bound", "sg_write_records", "sg_read_records", "sg_record_timing",
+    "sg_wire_bound", "sg_write_records", "sg_read_records", "sg_parse_records", "sg_record_timing",
     "sg_sha256", "sg_hmac_sha256", "sg_prf_new", "sg_prf_get_bytes", "sg_prf_free",
     "sg_derive_keys", "sg_finished_verify_data",
 ]
@@ -80,6 +80,13 @@ class SgReadResult(C.Structure):
 
     _fields_ = [("records", C.c_uint64), ("consumed", C.c_uint64), ("out_len", C.c_uint64),
                 ("error", C.c_int32), ("_pad", C.c_uint32)]
+
+
+class SgWireRecord(C.Structure):
+    """Mirror of ``struct sg_wire_record``."""
+
+    _fields_ = [("offset", C.c_uint64), ("frag_len", C.c_uint32), ("type", C.c_uint8), ("ver_major", C.c_uint8),
+                ("ver_minor", C.c_uint8), ("_pad", C.c_uint8)]
 
 
 SG_E_UNEXPECTED_MESSAGE = 3
@@ -162,6 +169,9 @@ def _declare(lib: C.CDLL) -> None:
     lib.sg_read_records.restype = C.c_int
     lib.sg_read_records.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t,
                                     C.c_void_p, C.c_void_p, C.c_size_t, C.POINTER(SgReadResult)]
+    lib.sg_parse_records.restype = C.c_int
+    lib.sg_parse_records.argtypes = [C.c_void_p, C.c_size_t, C.c_size_t, C.POINTER(SgWireRecord),
+                                     C.POINTER(C.c_size_t), C.POINTER(C.c_int32)]
     lib.sg_record_timing.restype = C.c_int
     lib.sg_record_timing.argtypes = [d, d, d, d]
     vp = C.c_void_p

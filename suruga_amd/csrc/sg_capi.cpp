@@ -44,10 +44,6 @@ namespace {
 using sg::fail;
 using sg::hip_fail;
 
-#ifndef SG_SINGLE_ZEROCOPY
-#define SG_SINGLE_ZEROCOPY 1
-#endif
-
 // A workspace of the library-owned cache.  Calls with no caller workspace
 // take one that no other call is enqueuing on, make their stream wait for its
 // previous user's work (`done`) and record `done` again after their launches,
@@ -372,8 +368,6 @@ sg_ctx* sg_ctx_new(const uint8_t key[32], int device) {
     const size_t cap_in = sg::kSingleInOff + SG_MAX_RECORD_LEN + 64;
     const size_t cap_out = sg::kSingleOutOff + SG_MAX_RECORD_LEN + 64;
     bool ok = hipMalloc((void**)&c->d_key, 64) == hipSuccess &&
-              hipMalloc((void**)&c->d_in, cap_in) == hipSuccess &&
-              hipMalloc((void**)&c->d_out, cap_out) == hipSuccess &&
               hipHostMalloc((void**)&c->h_in, cap_in, hipHostMallocDefault) == hipSuccess &&
               hipHostMalloc((void**)&c->h_out, cap_out, hipHostMallocDefault) == hipSuccess &&
               hipMalloc(&c->d_ws, sg_workspace_size(1)) == hipSuccess &&
@@ -393,8 +387,6 @@ void sg_ctx_free(sg_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     sg::record_staging_free(c->rec);
     (void)hipFree(c->d_key);
-    (void)hipFree(c->d_in);
-    (void)hipFree(c->d_out);
     (void)hipHostFree(c->h_in);
     (void)hipHostFree(c->h_out);
     (void)hipFree(c->d_ws);
@@ -419,17 +411,11 @@ static int single(sg_ctx* c, bool open, const uint8_t* nonce, size_t nonce_len, 
     std::memcpy(c->h_in, nonce, 8);
     if (adlen) std::memcpy(c->h_in + sg::kSingleAdOff, ad, adlen);
     if (in_len) std::memcpy(c->h_in + sg::kSingleInOff, in, in_len);
-    // SG_SINGLE_ZEROCOPY: the kernels read nonce | ad | record from the pinned
-    // block and write status | output into the pinned out block over PCIe (one
-    // record is a few KiB; two copy launches cost more than the transfer);
-    // otherwise one H2D and one D2H copy through device buffers
+    // the kernels read nonce | ad | record from the pinned block and write
+    // status | output into the pinned out block over PCIe (one record is a few
+    // KiB; two copy launches cost more than the transfer)
     uint8_t* src = c->h_in;
     uint8_t* dst = c->h_out;
-    if (!SG_SINGLE_ZEROCOPY) {
-        SG_HIP(hipMemcpyAsync(c->d_in, c->h_in, sg::kSingleInOff + in_len, hipMemcpyHostToDevice, c->stream));
-        src = c->d_in;
-        dst = c->d_out;
-    }
 
     sg_batch b;
     std::memset(&b, 0, sizeof b);
@@ -454,8 +440,6 @@ static int single(sg_ctx* c, bool open, const uint8_t* nonce, size_t nonce_len, 
     int rc = open ? sg_open_batch(&b) : sg_seal_batch(&b);
     if (rc != SG_OK) return rc;
     const size_t out_len = open ? n : n + SG_MAC_LEN;
-    if (!SG_SINGLE_ZEROCOPY)
-        SG_HIP(hipMemcpyAsync(c->h_out, c->d_out, sg::kSingleOutOff + out_len, hipMemcpyDeviceToHost, c->stream));
     SG_HIP(hipStreamSynchronize(c->stream));
     const uint8_t st = open ? c->h_out[0] : 0;
     if (open && st != 0) {

@@ -43,12 +43,10 @@ __device__ __forceinline__ void st16(void* p, u32x4 v) {
 #ifndef SG_STREAM_NT
 #define SG_STREAM_NT 1
 #endif
-#ifndef SG_DMA_POL
 #if SG_STREAM_NT
 #define SG_DMA_POL " nt"
 #else
 #define SG_DMA_POL ""
-#endif
 #endif
 __device__ __forceinline__ u32x4 gld16(const void* p) {
     const u32x4* q = reinterpret_cast<const u32x4*>(__builtin_assume_aligned(p, 16));

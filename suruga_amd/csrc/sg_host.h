@@ -44,9 +44,9 @@ struct DeviceGuard {
 // One context per direction (Aead::new_encryptor / new_decryptor): the key on
 // the device, staging for single records, and (lazily) the record-layer
 // pipeline of sg_write_records / sg_read_records.
-// Single-record staging (sg_seal / sg_open): one pinned host block and one
-// device block per direction, so a call is one H2D copy, the keying and AEAD
-// launches, and one D2H copy:
+// Single-record staging (sg_seal / sg_open): one pinned host block per
+// direction that the kernels read and write over the host link, so a call is
+// the keying and AEAD launches and one stream sync:
 //   in  block: nonce @0 | ad @kSingleAdOff | record @kSingleInOff
 //   out block: status @0 | output @kSingleOutOff
 namespace sg {
@@ -57,9 +57,8 @@ constexpr size_t kSingleOutOff = 64;
 struct sg_ctx {
     int device = 0;
     uint8_t* d_key = nullptr;      // 32 B
-    uint8_t* d_in = nullptr;       // kSingleInOff + SG_MAX_RECORD_LEN + 64
-    uint8_t* d_out = nullptr;      // kSingleOutOff + SG_MAX_RECORD_LEN + 64
-    uint8_t* h_in = nullptr;       // pinned mirrors of the two blocks
+    uint8_t* h_in = nullptr;       // pinned blocks the kernels read and write directly:
+                                   // kSingleInOff / kSingleOutOff + SG_MAX_RECORD_LEN + 64
     uint8_t* h_out = nullptr;
     void* d_ws = nullptr;
     hipStream_t stream = nullptr;

@@ -42,9 +42,6 @@
 #define SG_STR2(x) #x
 #define SG_STR(x) SG_STR2(x)
 
-#ifndef SG_SALU_PRE
-#define SG_SALU_PRE 1  // hoist the counter-free part of ChaCha round 1 to the SALU
-#endif
 
 namespace sg {
 namespace {
@@ -271,7 +268,7 @@ __device__ __forceinline__ void aead_record(const KParams& p, const uint32_t rec
         const bool vec_ok = (((uintptr_t)in | (uintptr_t)out) & 15u) == 0u;
         const uint32_t nblocks = (n + 63u) >> 6;
         ChaChaPre pre;
-        if constexpr (SG_SALU_PRE && L >= 64u) pre = chacha_pre(rk.k, rk.n14, rk.n15);
+        if constexpr (L >= 64u) pre = chacha_pre(rk.k, rk.n14, rk.n15);
         for (uint32_t b = t; b < nblocks; b += L) {
             const uint32_t off = b << 6;
             if (vec_ok && off + 64u <= n) {
@@ -279,7 +276,7 @@ __device__ __forceinline__ void aead_record(const KParams& p, const uint32_t rec
                 const u32x4 d2 = ld16(in + off + 32), d3 = ld16(in + off + 48);
                 uint32_t ks[16];
                 // data uses blocks 1.. (chacha20_poly1305.rs:52)
-                if constexpr (SG_SALU_PRE && L >= 64u) chacha_block_pre(ks, pre, rk.k, b + 1u, rk.n14, rk.n15);
+                if constexpr (L >= 64u) chacha_block_pre(ks, pre, rk.k, b + 1u, rk.n14, rk.n15);
                 else chacha_block(ks, rk.k, b + 1u, rk.n14, rk.n15);
                 const u32x4 r0 = d0 ^ u32x4{ks[0], ks[1], ks[2], ks[3]};
                 const u32x4 r1 = d1 ^ u32x4{ks[4], ks[5], ks[6], ks[7]};
@@ -303,7 +300,7 @@ __device__ __forceinline__ void aead_record(const KParams& p, const uint32_t rec
             } else {
                 // partial last block or misaligned record: byte granular
                 uint32_t ks[16];
-                if constexpr (SG_SALU_PRE && L >= 64u) chacha_block_pre(ks, pre, rk.k, b + 1u, rk.n14, rk.n15);
+                if constexpr (L >= 64u) chacha_block_pre(ks, pre, rk.k, b + 1u, rk.n14, rk.n15);
                 else chacha_block(ks, rk.k, b + 1u, rk.n14, rk.n15);
 #pragma unroll
                 for (uint32_t w = 0; w < 16; ++w) {
@@ -1046,8 +1043,7 @@ hipError_t launch_compare(const uint8_t* a, uint64_t sa, const uint8_t* b, uint6
 }
 
 const char* class_kernel_config() {
-    return "sg_aead_kernel v9/salu_pre=" SG_STR(SG_SALU_PRE)
-           ": 8 size classes (2..256 lanes per record, one 64-B block per lane, device bucketing, exact class grids), "
+    return "sg_aead_kernel v9 8 size classes (2..256 lanes per record, one 64-B block per lane, device bucketing, exact class grids), "
            "lane=64B ChaCha block (counter-free round-1 QRs on SALU for wave-uniform records), Poly1305 contiguous-chunk "
            "Horner radix-2^32 (clamped r, unaligned 16-B LDS block loads, folded pad bit) on min(L,64) lanes + per-lane "
            "r^(k(PL-1-t)) scale + DPP sum, tag finalised on the SALU for one-record waves, keying pre-pass";

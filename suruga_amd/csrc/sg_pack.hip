@@ -84,20 +84,10 @@ namespace {
 
 using namespace dev;
 
-#ifndef SG_PACK_NT_LD
-#define SG_PACK_NT_LD 0
-#endif
-#ifndef SG_PACK_NT_ST
-#define SG_PACK_NT_ST 0
-#endif
-__device__ __forceinline__ u32x4 pld16(const void* p) { return SG_PACK_NT_LD ? gld16(p) : ld16(p); }
-__device__ __forceinline__ void pst16(void* p, u32x4 v) {
-    if constexpr (SG_PACK_NT_ST) gst16(p, v); else st16(p, v);
-}
-
-#ifndef SG_PACK_IDLE_BARRIERS
-#define SG_PACK_IDLE_BARRIERS 1
-#endif
+// the packed kernel's lanes each move their own 64-byte block: default cache
+// policy (the non-temporal one measured -1.3 % on C2, round 3)
+__device__ __forceinline__ u32x4 pld16(const void* p) { return ld16(p); }
+__device__ __forceinline__ void pst16(void* p, u32x4 v) { st16(p, v); }
 
 constexpr uint32_t kPackRecs = 128;                // records per workgroup run
 constexpr uint32_t kPackWaves = 8;                 // two per SIMD: lock-step pairs
@@ -121,7 +111,7 @@ constexpr uint32_t kSCtot = 22;   // constant term (5 limbs)
 constexpr uint32_t kSNb = 27, kSStart = 28, kSRec = 29;
 static_assert(kSRec < kSlotWords, "slot layout");
 
-// Per-record MAC accumulator (SG_PACK_ACC64, default on): the lane terms
+// Per-record MAC accumulator: the lane terms
 // fmul(Q, W) go in unreduced -- limbs 0, 2, 3, 4 < 2^26 (64 of them stay below
 // 2^32), limb 1 < 2^26 + 2^7 summed as 64 bits -- instead of through a full
 // carry ripple per lane (~30 VALU per chunk; round 4).  Three 64-bit LDS
@@ -130,10 +120,7 @@ static_assert(kSRec < kSlotWords, "slot layout");
 // same-address atomics of the lanes of one record serialise, so fewer
 // instructions cost fewer conflict cycles (five u32 atomics measured 0.7 %
 // slower on C2, r04u).
-#ifndef SG_PACK_ACC64
-#define SG_PACK_ACC64 1
-#endif
-constexpr uint32_t kAccWords = SG_PACK_ACC64 ? 6u : 5u;  // v0 v2 v3 v4 | v1 (u64)  or  v0..v4
+constexpr uint32_t kAccWords = 6u;  // (v0, v2) u64 | (v3, v4) u64 | v1 u64
 struct PackLds {
     uint32_t slot[kPackRecs * kSlotWords];
     uint32_t tab[kPackRecs * kTabWords];
@@ -341,12 +328,12 @@ __device__ __forceinline__ void pack_run(const KParams& p, const uint32_t* __res
     // SIMD), so that in the last, partial round the chunks go to whole pairs
     // and the waves without one only keep the barrier count (s_barrier, no
     // VALU): their issue slots go to the CU's other workgroups, and the working
-    // waves stay paired (SG_PACK_IDLE_BARRIERS; round 2 measured that idle waves
-    // running the rounds with EXEC off save only power).
+    // waves stay paired (round 2 measured that idle waves running the rounds
+    // with EXEC off save only power).
     const uint32_t pos = 2u * (wave & 3u) + (wave >> 2);
     for (uint32_t k = 0; k < nrounds; ++k) {
-        const uint32_t c = kPackWaves * k + (SG_PACK_IDLE_BARRIERS ? pos : wave);
-        if (SG_PACK_IDLE_BARRIERS && c >= nchunks) {  // (wave-uniform) no chunk in this round
+        const uint32_t c = kPackWaves * k + pos;
+        if (c >= nchunks) {  // (wave-uniform) no chunk in this round
             // as many barriers as the ten double rounds of a working wave
             asm volatile(".rept " SG_PACK_STR(SG_PACK_IDLE_BARS) "\ns_barrier\n.endr" ::: "memory");
             continue;
@@ -415,21 +402,12 @@ __device__ __forceinline__ void pack_run(const KParams& p, const uint32_t* __res
             const uint32_t* tb = L.tab + m * kTabWords;
             const F26 W = tab_weight(tb, i);
             uint32_t* ac = L.acc + kAccWords * m;
-            if constexpr (SG_PACK_ACC64) {
-                const F26 t = fmul(Q, W);
-                atomicAdd(reinterpret_cast<unsigned long long*>(ac + 0),
-                          (unsigned long long)t.v0 | ((unsigned long long)t.v2 << 32));
-                atomicAdd(reinterpret_cast<unsigned long long*>(ac + 2),
-                          (unsigned long long)t.v3 | ((unsigned long long)t.v4 << 32));
-                atomicAdd(reinterpret_cast<unsigned long long*>(ac + 4), (unsigned long long)t.v1);
-            } else {
-                const F26 t = ripple_full(fmul(Q, W));
-                atomicAdd(ac + 0, t.v0);
-                atomicAdd(ac + 1, t.v1);
-                atomicAdd(ac + 2, t.v2);
-                atomicAdd(ac + 3, t.v3);
-                atomicAdd(ac + 4, t.v4);
-            }
+            const F26 t = fmul(Q, W);
+            atomicAdd(reinterpret_cast<unsigned long long*>(ac + 0),
+                      (unsigned long long)t.v0 | ((unsigned long long)t.v2 << 32));
+            atomicAdd(reinterpret_cast<unsigned long long*>(ac + 2),
+                      (unsigned long long)t.v3 | ((unsigned long long)t.v4 << 32));
+            atomicAdd(reinterpret_cast<unsigned long long*>(ac + 4), (unsigned long long)t.v1);
         }
     }
     SG_STAMP(0u, 3);
@@ -442,11 +420,10 @@ __device__ __forceinline__ void pack_run(const KParams& p, const uint32_t* __res
         const uint32_t* sl = L.slot + m0 * kSlotWords;
         const uint32_t n = 64u * sl[kSNb], rec = sl[kSRec];
         const uint32_t* ac = L.acc + kAccWords * m0;
-        // (ACC64: v1 = lo + hi 2^32 -> hi 2^58 = (hi << 6) 2^52 joins limb 2 after
-        // the first carry pass: limb 2's raw sum can reach 2^32 - 64, and hi <= 1)
-        F26 f = SG_PACK_ACC64 ? carry1(F26{ac[0], ac[4], ac[1], ac[2], ac[3]})
-                              : carry1(F26{ac[0], ac[1], ac[2], ac[3], ac[4]});
-        if constexpr (SG_PACK_ACC64) f.v2 += ac[5] << 6;
+        // (v1 = lo + hi 2^32 -> hi 2^58 = (hi << 6) 2^52 joins limb 2 after the
+        // first carry pass: limb 2's raw sum can reach 2^32 - 64, and hi <= 1)
+        F26 f = carry1(F26{ac[0], ac[4], ac[1], ac[2], ac[3]});
+        f.v2 += ac[5] << 6;
         f = carry1(f26_add(f, load_f26(sl + kSCtot)));
         const uint32_t s[4] = {sl[kSS + 0], sl[kSS + 1], sl[kSS + 2], sl[kSS + 3]};
         uint32_t tw[4];
@@ -514,15 +491,12 @@ extern "C" int sg_pack_profile_read(unsigned long long* host, size_t n) {
 }
 #endif
 
-#ifndef SG_PACK_DEFAULT
-#define SG_PACK_DEFAULT 1
-#endif
 static int g_pack = -1;  // -1: not read from the environment yet
 bool pack_enabled() {
     if (__atomic_load_n(&g_pack, __ATOMIC_ACQUIRE) < 0) {
         const char* e = getenv("SG_PACK");
         int expect = -1;
-        __atomic_compare_exchange_n(&g_pack, &expect, e ? (e[0] == '1' ? 1 : 0) : (SG_PACK_DEFAULT ? 1 : 0), false,
+        __atomic_compare_exchange_n(&g_pack, &expect, e ? (e[0] == '1' ? 1 : 0) : 1, false,
                                     __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE);
     }
     return __atomic_load_n(&g_pack, __ATOMIC_ACQUIRE) == 1;

@@ -80,7 +80,6 @@ constexpr uint32_t kWprWgLds = kWprWaves * kWprWaveLds + 16;
 static_assert(2 * kWprWgLds <= 160 * 1024, "two workgroups per CU");
 static_assert(kWprDescWords * 4 <= 48, "descriptor slot");
 constexpr uint32_t kWprKeyThreads = 64;
-constexpr uint32_t kWprKeyStride = 81;      // LDS words per record and half
 
 // Geometry of the MAC stream ad || le64(|ad|) || ct || le64(n), n a multiple
 // of 16 (C1: n = 2^14).  A record of n < 2^14 bytes runs right-aligned in the
@@ -105,23 +104,6 @@ __device__ __forceinline__ WprGeom wpr_geom(uint32_t adlen, uint32_t n) {
     return g;
 }
 
-// sum_{i=1..m} x^i and x^m (geo_sum of sg_device.h, also returning the power)
-__device__ __forceinline__ F26 geo_sum_pow(const F26 x, const uint32_t m, F26* pw_out) {
-    F26 g = f26_zero(), pw = f26_one();
-    if (m != 0u) {
-        for (int bit = 31 - __builtin_clz(m); bit >= 0; --bit) {
-            g = mul_add(g, pw.v0, pw.v1, pw.v2, pw.v3, pw.v4, g);
-            pw = fmul(pw, pw);
-            if ((m >> bit) & 1u) {
-                pw = fmul(pw, x);
-                g = f26_add(g, pw);
-            }
-        }
-    }
-    *pw_out = pw;
-    return g;
-}
-
 // bytes >= lo of a little-endian word set: mask of the bytes whose index
 // (4 w + byte) is >= lo
 __device__ __forceinline__ uint32_t bytes_from(uint32_t w, uint32_t lo) {
@@ -134,40 +116,23 @@ __device__ __forceinline__ uint32_t bytes_from(uint32_t w, uint32_t lo) {
 // accumulator, negated (tests/test_wpr_mac_model.py: CJ)
 constexpr uint32_t kCJ0 = 0x1bd2d2bu, kCJ1 = 0x36f6f6fu, kCJ2 = 0x3dbdbdbu, kCJ3 = 0x2f6f6f6u, kCJ4 = 0x1bdbdbdu;
 
-#ifndef SG_WPR_GEO_TABLES
-#define SG_WPR_GEO_TABLES 1  // bucket keying: geometric sums from the power tables (0: square-and-multiply)
-#endif
-
 // ---------------------------------------------------------------------------
 // Keying pre-pass: one lane per record, 64 records per wave, the 160-word
-// record (sg_internal.h, kW*) staged in LDS by halves and stored coalesced.
+// record (sg_internal.h, kW*) stored unit by unit from registers (grouped layout below).
 // LIST: lane = slot of a bucket list (record wl.list[slot], any n of the
 // bucket), which also writes the slot's descriptor; otherwise slot = record
 // and n = 2^14.
 // ---------------------------------------------------------------------------
-// Table layout in HBM: SG_WPR_TAB_SPLIT (default) stores the two halves of the
-// launch's records as two arrays, half h of slot s at tab + h (count 80) + 80 s,
-// so that a workgroup's flush of one half is one contiguous run of 64 x 320
-// bytes (whole 128-byte lines); SG_WPR_TAB_NT writes them non-temporal, so the
-// table does not sit dirty in the caches while the record kernel streams.
-#ifndef SG_WPR_TAB_SPLIT
-#define SG_WPR_TAB_SPLIT 1
-#endif
-#ifndef SG_WPR_TAB_NT
-#define SG_WPR_TAB_NT 1
-#endif
-// SG_WPR_TAB_GROUPED (default): the records of eight consecutive slots (a
+// Table layout in HBM (round 3): the records of eight consecutive slots (a
 // record kernel's group) interleaved by 16-byte unit, unit u of slot 8 g + w
 // at tab + 1280 g + 4 (u rows + w) words (rows = 8, or count mod 8 in the last
-// group).  Each lane then stores its own record unit by unit straight from
-// registers and every store instruction still writes whole 128-byte lines (a
-// group's row of one unit), so the keying kernel needs no LDS staging and runs
-// at the occupancy its registers allow; the record kernel's 40 unit reads per
-// record touch lines that the other seven waves of its group read at the same
-// time (the same 640 bytes per record from HBM).
-#ifndef SG_WPR_TAB_GROUPED
-#define SG_WPR_TAB_GROUPED 1
-#endif
+// group).  Each lane stores its own record unit by unit straight from
+// registers (non-temporal: the table does not sit dirty in the caches while
+// the record kernel streams) and every store instruction still writes whole
+// 128-byte lines (a group's row of one unit), so the keying kernel needs no
+// LDS staging and runs at the occupancy its registers allow; the record
+// kernel's 40 unit reads per record touch lines that the other seven waves of
+// its group read at the same time (the same 640 bytes per record from HBM).
 __device__ __forceinline__ uint32_t* wpr_tab_unit(const WprList& wl, uint32_t slot, uint32_t u) {
     const uint32_t g = slot >> 3, w = slot & 7u;
     const uint32_t rows = g < (wl.count >> 3) ? 8u : (wl.count & 7u);
@@ -180,33 +145,7 @@ __device__ __forceinline__ void wpr_store_units(const WprList& wl, uint32_t slot
 #pragma unroll
     for (uint32_t u = U0; u < U1; ++u) {
         const u32x4 val = {rec[4u * u], rec[4u * u + 1u], rec[4u * u + 2u], rec[4u * u + 3u]};
-        u32x4* dst = reinterpret_cast<u32x4*>(wpr_tab_unit(wl, slot, u));
-        if constexpr (SG_WPR_TAB_NT) {
-            __builtin_nontemporal_store(val, dst);
-        } else {
-            st16(dst, val);
-        }
-    }
-}
-__device__ __forceinline__ uint32_t* wpr_tab_half(const WprList& wl, uint32_t slot, uint32_t half) {
-    if constexpr (SG_WPR_TAB_SPLIT) return wl.tab + (uint64_t)half * wl.count * 80u + (uint64_t)slot * 80u;
-    return wl.tab + (uint64_t)slot * kWprRecWords + 80u * half;
-}
-__device__ __forceinline__ void wpr_flush_half(const WprList& wl, uint32_t slot0, uint32_t half, const uint32_t* stage,
-                                               uint32_t lane) {
-    const uint32_t nrec = wl.count - slot0 < kWprKeyThreads ? wl.count - slot0 : kWprKeyThreads;
-    const uint32_t nvec = nrec * 20u;  // 80 words = 20 x 16 B per record and half
-    uint32_t* dst0 = wpr_tab_half(wl, slot0, half);
-    for (uint32_t v = lane; v < nvec; v += kWprKeyThreads) {
-        const uint32_t rr = v / 20u, c = v - rr * 20u;
-        const uint32_t* src = stage + rr * kWprKeyStride + 4u * c;
-        const u32x4 val = {src[0], src[1], src[2], src[3]};
-        uint32_t* dst = SG_WPR_TAB_SPLIT ? dst0 + 4u * v : wpr_tab_half(wl, slot0 + rr, half) + 4u * c;
-        if constexpr (SG_WPR_TAB_NT) {
-            __builtin_nontemporal_store(val, reinterpret_cast<u32x4*>(dst));
-        } else {
-            st16(dst, val);
-        }
+        __builtin_nontemporal_store(val, reinterpret_cast<u32x4*>(wpr_tab_unit(wl, slot, u)));
     }
 }
 
@@ -217,15 +156,10 @@ struct WprKeyJobs {
     uint32_t njobs;
 };
 
-#ifndef SG_WPR_KEY_WAVES
-#define SG_WPR_KEY_WAVES 2  // waves per SIMD the keying kernel is compiled for (4 and more spill to scratch)
-#endif
+// (compiled for two waves per SIMD: four and more spill to scratch)
 template <bool OPEN, bool LIST>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SG_WPR_KEY_WAVES))) void sg_wpr_keying_kernel(
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void sg_wpr_keying_kernel(
     const KParams p, const WprKeyJobs jobs) {
-#if !SG_WPR_TAB_GROUPED
-    __shared__ uint32_t stage[kWprKeyThreads * kWprKeyStride];
-#endif
     const uint32_t lane = threadIdx.x;
     WprList wl = jobs.b[0];
     uint32_t b0 = 0;
@@ -237,14 +171,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SG_WPR_KEY_W
         }
     const uint32_t slot0 = (blockIdx.x - b0) * kWprKeyThreads;
     const uint32_t slot = slot0 + lane;
-#if SG_WPR_TAB_GROUPED
     uint32_t rbuf[kWprRecWords];  // the lane's record (registers once unrolled)
 #pragma unroll
     for (uint32_t i = 0; i < kWprRecWords; ++i) rbuf[i] = 0u;
     uint32_t* st = rbuf + 80;  // the second half first (offsets below are half-relative)
-#else
-    uint32_t* st = stage + lane * kWprKeyStride;
-#endif
     const uint32_t adlen = p.tls ? 13u : p.ad_len;
     if (blockIdx.x == b0 && lane == 0u) *wl.ctr = 0u;  // the record kernel's group counter
 
@@ -308,14 +238,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SG_WPR_KEY_W
         y = fmul(y, R8);
     }
     const F26 T = y;  // R^32 = r^128
-#if SG_WPR_TAB_GROUPED
     wpr_store_units<20, 40>(wl, slot, act, rbuf);
     st = rbuf;
-#else
-    __syncthreads();
-    wpr_flush_half(wl, slot0, 1u, stage, lane);
-    __syncthreads();
-#endif
 
     // ---- first half: s, ctot, rd[u] = r^(1 + delta + u), tk[k] = T^k ----
     st[kWS + 0] = s[0]; st[kWS + 1] = s[1]; st[kWS + 2] = s[2]; st[kWS + 3] = s[3];
@@ -335,9 +259,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SG_WPR_KEY_W
         t = fmul(t, T);
         if constexpr (LIST) ta = sel((uint32_t)k + 1u == ca, t, ta);            // T^a
     }
-#if SG_WPR_TAB_GROUPED
     wpr_store_units<3, 20>(wl, slot, act, rbuf);  // rd and tk now; s and ctot (units 0-2) at the end
-#endif
 
     // geometric sums: SW = sum_{u<32} R^u; g = G(m) = sum_{i=1..m} r^i and rm = r^m
     // (m = n / 16: for n = 2^14, G(1024) = (r + r^2 + r^3 + r^4) SW sum_k T^k, r^1024 = T^8).
@@ -348,9 +270,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SG_WPR_KEY_W
     const F26 SW = fmul(carry1(sum_hi), carry1(sum_lo));
     const F26 G4 = carry1(f26_add(f26_add(r, r2), f26_add(r3, R)));
     F26 g, rm;
-    if constexpr (LIST && !SG_WPR_GEO_TABLES) {
-        g = geo_sum_pow(r, G.m, &rm);
-    } else if constexpr (LIST) {
+    if constexpr (LIST) {
         const F26 Sc = fmul_add(yc, carry1(plo), fmul(carry1(phi), carry1(sum_lo)));
         const F26 Sk = fmul_add(SW, carry1(pta), fmul(ta, Sc));
         g = fmul(G4, Sk);
@@ -420,12 +340,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SG_WPR_KEY_W
     }
     const F26 ctot = carry1(f26_add(f26_add(f26_add(pads, bias), f26_add(seed, prefix)), suffix));
     store_f26(st + kWCtot, ctot);
-#if SG_WPR_TAB_GROUPED
     wpr_store_units<0, 3>(wl, slot, act, rbuf);
-#else
-    __syncthreads();
-    wpr_flush_half(wl, slot0, 0u, stage, lane);
-#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -516,11 +431,8 @@ __device__ unsigned long long g_wpr_prof[kProfWaves][kProfPhases];
 #define SG_ACC(k, a, b)
 #endif
 
-// The double-round body (experiment builds may pick another barrier spacing
-// from tools/chacha_grp.inc; every form computes the same rounds)
-#ifndef SG_WPR_DR_ASM
+// The double-round body: grouped ARX with an s_barrier after every rotate group
 #define SG_WPR_DR_ASM SG_CHACHA_DR_NB1_BAR1
-#endif
 
 // A zero vector materialised where it is used (a hoisted constant would hold
 // four VGPRs across the whole record loop).
@@ -553,7 +465,7 @@ __device__ __forceinline__ void dma_sv(uint32_t l0, const void* sbase, uint32_t 
                  : "memory");
 }
 
-// Address forms of the output path (SG_WPR_ADDR, default on): the staged
+// Address forms of the output path (round 4): the staged
 // output is read from LDS through one VGPR base (the lane's swizzled unit in
 // the wave's slice) with the buffer and piece as immediate offsets, and stored
 // with the saddr form of global_store (record base in SGPRs, the lane's 16-byte
@@ -561,13 +473,6 @@ __device__ __forceinline__ void dma_sv(uint32_t l0, const void* sbase, uint32_t 
 // address arithmetic runs per piece.  The stores are asm: their vmcnt is
 // counted by the kernel's own waits like the DMAs' (s_nop: no VALU may
 // overwrite the data registers of a >64-bit store in the next cycle).
-#ifndef SG_WPR_ADDR
-#define SG_WPR_ADDR 1
-#endif
-// digit lines from the unreduced product limbs (round 4; 0: carry ripple first)
-#ifndef SG_WPR_DIGIT_MAD
-#define SG_WPR_DIGIT_MAD 1
-#endif
 typedef const __attribute__((address_space(3))) u32x4* lu128p;
 template <uint32_t OFF>
 __device__ __forceinline__ void gst16_s(const void* sbase, uint32_t voff, const u32x4& v) {
@@ -633,9 +538,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     asm volatile("" : "+v"(mac_lo_a), "+v"(mac_hi_a));
     const lu32p mac_lo = (lu32p)(uintptr_t)mac_lo_a, mac_hi = (lu32p)(uintptr_t)mac_hi_a;
     // output read-out base (the lane's swizzled unit of the wave's slice) and the
-    // lane's byte offset of a lane-contiguous 1 KiB piece (SG_WPR_ADDR)
+    // lane's byte offset of a lane-contiguous 1 KiB piece
     // (uniform 16 KiB launches only: the bucket kernels have no VGPRs to spare)
-    constexpr bool kAddr = SG_WPR_ADDR && !LIST;
+    constexpr bool kAddr = !LIST;
     uint32_t ob_a = (uint32_t)(uintptr_t)(buf + 16u * wunit), lane16 = 16u * lane;
     if constexpr (kAddr) asm volatile("" : "+v"(ob_a), "+v"(lane16));
     const lu128p ob_base = (lu128p)(uintptr_t)ob_a;
@@ -706,10 +611,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     };
     auto dma_table_of = [&](uint32_t slot) {  // into the line area, lane u: unit u
         if (lane < kWprRecWords / 4u) {
-            if constexpr (SG_WPR_TAB_GROUPED)
-                dma_one(lds_lines, wpr_tab_unit(wl, slot, lane));
-            else
-                dma_one(lds_lines, wpr_tab_half(wl, slot, lane >= 20u ? 1u : 0u) + 4u * (lane >= 20u ? lane - 20u : lane));
+            dma_one(lds_lines, wpr_tab_unit(wl, slot, lane));
         }
     };
     auto dma_desc_of = [&](uint32_t slot) {  // LIST: into the descriptor slot
@@ -833,14 +735,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
             // ripple_full form took ~35 more VALU per record)
             uint32_t c;  // digits = the bytes of X + 0x80..80, each ^ 0x80
             uint32_t d[5];
-#if !SG_WPR_DIGIT_MAD
-            const F26 v = ripple_full(lv);
-            d[0] = addc(v.v0 | (v.v1 << 26), 0x80808080u, 0u, &c) ^ 0x80808080u;
-            d[1] = addc((v.v1 >> 6) | (v.v2 << 20), 0x80808080u, c, &c) ^ 0x80808080u;
-            d[2] = addc((v.v2 >> 12) | (v.v3 << 14), 0x80808080u, c, &c) ^ 0x80808080u;
-            d[3] = addc((v.v3 >> 18) | (v.v4 << 8), 0x80808080u, c, &c) ^ 0x80808080u;
-            d[4] = ((v.v4 >> 24) + 0x80u + c) ^ 0x80u;
-#else
             uint64_t t = mad_u64_u32(lv.v1, 1u << 26, (uint64_t)lv.v0);
             const uint32_t x0 = (uint32_t)t;
             t = mad_u64_u32(lv.v2, 1u << 20, t >> 32);
@@ -853,7 +747,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
             d[2] = addc(x2, 0x80808080u, c, &c) ^ 0x80808080u;
             d[3] = addc((uint32_t)t, 0x80808080u, c, &c) ^ 0x80808080u;
             d[4] = ((uint32_t)(t >> 32) + 0x80u + c) ^ 0x80u;
-#endif
             uint8_t* ln = lines + kWprLineBytes * lane;
             const u32x4 z = zero4();
             if constexpr (TLS) {
@@ -1357,15 +1250,12 @@ hipError_t launch_wpr_list(const KParams& p, bool open, uint32_t J, const WprLis
     return hipGetLastError();
 }
 
-#ifndef SG_WPR_DEFAULT
-#define SG_WPR_DEFAULT 1
-#endif
 static int g_wpr = -1;  // -1: not read from the environment yet
 bool wpr_enabled() {
     if (__atomic_load_n(&g_wpr, __ATOMIC_ACQUIRE) < 0) {
         const char* e = getenv("SG_LOCKSTEP");
         int expect = -1;
-        __atomic_compare_exchange_n(&g_wpr, &expect, e ? (e[0] == '1' ? 1 : 0) : (SG_WPR_DEFAULT ? 1 : 0), false,
+        __atomic_compare_exchange_n(&g_wpr, &expect, e ? (e[0] == '1' ? 1 : 0) : 1, false,
                                     __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE);
     }
     return __atomic_load_n(&g_wpr, __ATOMIC_ACQUIRE) == 1;

@@ -253,3 +253,39 @@ def test_gpu_per_record_reader(gpu, oracle):
         r.read_record()
     assert e.value.kind is TlsErrorKind.BadRecordMac
     assert struct.pack(">Q", r.read_count) == bytes(7) + b"\x02"
+
+
+def test_parse_records_header_checks_cpu():
+    """sg_parse_records (host only, no GPU call): the header checks of
+    sg_read_records in TlsReader::read_record's order (tls.rs:218-238,
+    258-262, 269-272) on the reference's own reader cases, called through the
+    C ABI on the CPU.  (The same parser runs under ASan/UBSan over a corpus in
+    tests/test_sanitizers.py.)"""
+    import ctypes as C
+
+    from suruga_amd import _native as N
+
+    lib = N.load()
+
+    def parse(wire: bytes, max_records: int = 64):
+        recs = (N.SgWireRecord * max_records)()
+        count, err = C.c_size_t(0), C.c_int32(0)
+        buf = (C.c_uint8 * max(len(wire), 1)).from_buffer_copy(wire or b"\0")
+        N.check(lib.sg_parse_records(buf, len(wire), max_records, recs, C.byref(count), C.byref(err)))
+        return [(r.offset, r.frag_len, r.type, r.ver_major, r.ver_minor) for r in recs[:count.value]], err.value
+
+    def rec(t, n, fill=0xAB):
+        return bytes([t, 3, 3, n >> 8, n & 0xFF]) + bytes([fill]) * n
+
+    two = rec(23, 16) + rec(22, 300)
+    assert parse(two) == ([(5, 16, 23, 3, 3), (26, 300, 22, 3, 3)], N.SG_OK)
+    assert parse(two, 1) == ([(5, 16, 23, 3, 3)], N.SG_OK)             # max_records
+    assert parse(two[:-1]) == ([(5, 16, 23, 3, 3)], N.SG_OK)           # incomplete: wait for bytes
+    assert parse(rec(23, 16) + bytes([0x18, 3, 3, 0, 3, 1, 0, 0x20])) == \
+        ([(5, 16, 23, 3, 3)], N.SG_E_UNEXPECTED_MESSAGE)               # tls.rs test_reader_unknown
+    big = ENC_RECORD_MAX_LEN + 1
+    assert parse(bytes([0x17, 3, 3, big >> 8, big & 0xFF]))[1] == N.SG_E_RECORD_OVERFLOW  # header alone suffices
+    assert parse(rec(23, 15))[1] == N.SG_E_SHORT                        # < mac_len (tls.rs:258-262)
+    assert parse(rec(23, RECORD_MAX_LEN + 17))[1] == N.SG_E_RECORD_OVERFLOW  # decrypted > 2^14 (:269-272)
+    assert parse(rec(23, RECORD_MAX_LEN + 16)) == ([(5, RECORD_MAX_LEN + 16, 23, 3, 3)], N.SG_OK)
+    assert parse(b"") == ([], N.SG_OK)

@@ -1,5 +1,5 @@
 """The wave-per-record keying table's grouped layout (sg_wpr.hip,
-wpr_tab_unit, SG_WPR_TAB_GROUPED): restated here and checked to be a
+wpr_tab_unit): restated here and checked to be a
 bijection from (slot, unit, word) onto the count x 160 words the workspace
 reserves, for full and partial last groups, and to give every store
 instruction of the keying kernel (unit u of 64 consecutive slots) whole

@@ -13,10 +13,10 @@ for i in $(seq 1 "$R"); do
   for spec in "$@"; do
     name=${spec%%=*}; lib=${spec#*=}
     if [ "$lib" = "-" ]; then lib=suruga_amd/libsuruga_gpu.so; fi
-    SURUGA_ALLOW_VARIANT=1 SURUGA_GPU_LIB=$lib timeout -k 10 300 python bench.py --no-cpu-baseline --no-bitexact --steps 10 ${BENCH_ARGS:-} > "$OUT/${name}_$i.json"
+    SURUGA_ALLOW_VARIANT=1 SURUGA_GPU_LIB=$lib timeout -k 10 300 python bench.py --no-cpu-baseline --no-bitexact --steps 10 --c2-steps 0 ${BENCH_ARGS:-} > "$OUT/${name}_$i.json"
     rc=$?
     # rc 3 = ran but not correct: accepted for timing-only variants (AB_ALLOW_WRONG=1)
     if [ $rc -ne 0 ] && ! { [ $rc -eq 3 ] && [ "${AB_ALLOW_WRONG:-0}" = 1 ]; }; then echo "$name rc=$rc"; exit $rc; fi
-    python -c "import json; d=json.loads(open('$OUT/${name}_$i.json').read().strip().splitlines()[-1]); print('$name', '$i', d['value'], 'seal', d['kernel_ms']['seal'], 'open', d['kernel_ms']['open'], 'keying', d['kernel_ms']['keying'], 'correct', d['correct'])"
+    python -c "import json; d=json.loads(open('$OUT/${name}_$i.json').read().strip().splitlines()[-1]); e=d.get('energy') or {}; print('$name', '$i', d['value'], 'seal', d['kernel_ms']['seal'], 'open', d['kernel_ms']['open'], 'keying', d['kernel_ms']['keying'], 'correct', d['correct'], 'W', e.get('board_power_w'), 'MHz', e.get('sclk_mhz'), 'uJ', e.get('seal_uj_per_record'), e.get('open_uj_per_record'))"
   done
 done
