@@ -12,12 +12,16 @@
 //   TlsReader::read_message   tls.rs:294-348  (handshake messages returned raw:
 //       the handshake is outside this path)
 //   RecordStreamReader        batched read_record: one sg_read_records per buffer.
+//   HostBuffer                registered (sg_host_register) caller buffers: the
+//       record layer's zero-copy path; complete_records: the header walk alone.
 #ifndef SURUGA_TLS_HPP
 #define SURUGA_TLS_HPP
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
+#include <new>
 #include <memory>
 #include <string>
 #include <utility>
@@ -332,6 +336,52 @@ private:
     std::vector<uint8_t> types_;
     std::vector<uint32_t> lens_;
 };
+
+// Page-locked caller buffer for the record layer's zero-copy path: memory
+// registered with sg_host_register moves by DMA straight between it and the
+// device (sg_write_records' data and wire, sg_read_records' wire and out).
+// register_it = false gives the same buffer unregistered (the staged path).
+class HostBuffer {
+public:
+    HostBuffer(size_t n, bool register_it) : n_(n) {
+        p_ = static_cast<uint8_t*>(std::aligned_alloc(4096, (n + 4095) / 4096 * 4096));
+        if (!p_) throw std::bad_alloc();
+        if (register_it) {
+            const int rc = sg_host_register(p_, n_);
+            if (rc != SG_OK) {
+                std::free(p_);
+                check_sg(rc);
+            }
+            reg_ = true;
+        }
+    }
+    ~HostBuffer() {
+        if (reg_) (void)sg_host_unregister(p_);
+        std::free(p_);
+    }
+    HostBuffer(const HostBuffer&) = delete;
+    HostBuffer& operator=(const HostBuffer&) = delete;
+    uint8_t* data() const { return p_; }
+    size_t size() const { return n_; }
+    bool registered() const { return reg_; }
+
+private:
+    uint8_t* p_ = nullptr;
+    size_t n_ = 0;
+    bool reg_ = false;
+};
+
+// Bytes of `wire` taken by its complete records (tls.rs:217-238 header checks,
+// sg_parse_records; host only): the rest is a partial record to carry over.
+// Throws the first bad header's TlsError.
+inline size_t complete_records(const uint8_t* wire, size_t n, size_t max_records = 4096) {
+    std::vector<sg_wire_record> recs(max_records);
+    size_t count = 0;
+    int32_t error = SG_OK;
+    check_sg(sg_parse_records(wire, n, recs.size(), recs.data(), &count, &error));
+    if (error != SG_OK && count == 0) throw detail::record_error(error);
+    return count ? recs[count - 1].offset + recs[count - 1].frag_len : 0;
+}
 
 }  // namespace suruga
 

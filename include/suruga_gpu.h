@@ -210,6 +210,20 @@ int sg_open_batch(const sg_batch* b);
                                       decrypted fragment > 2^14 (tls.rs:269-272,
                                       where the reference panics)                  */
 
+/* Caller buffers for the record layer's zero-copy path: page-locks [p, p+len)
+ * (hipHostRegister) and records the range.  When sg_write_records' `data` and
+ * `wire`, or sg_read_records' `wire` and `out`, both lie inside registered
+ * ranges, the record bytes move by DMA straight between those buffers and the
+ * device -- no framing copy through the library's pinned staging (the
+ * 5-byte headers are written / parsed by the host; sg_read_records takes the
+ * zero-copy path for chunks of equal, back-to-back records and clears the
+ * plaintext of a failed record and of every record after it in `out`, as it
+ * delivers none of them).  Unregister only when no call uses the range.
+ * SG_ZERO_COPY=0 in the environment disables the path.  SG_OK or SG_E_ARG /
+ * SG_E_HIP. */
+int sg_host_register(void* p, size_t len);
+int sg_host_unregister(void* p);
+
 /* Upper bound of the wire bytes sg_write_records produces for len bytes. */
 size_t sg_wire_bound(size_t len);
 

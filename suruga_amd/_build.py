@@ -168,11 +168,31 @@ def build_ossl(force: bool = False):
     return OSSL_LIB
 
 
+LOOPBACK_SRC = ROOT / "tools" / "loopback_cpp.cpp"
+LOOPBACK_BIN = ROOT / "tools" / "loopback_cpp"
+
+
+def build_loopback_cpp(force: bool = False) -> Path:
+    """tools/loopback_cpp: C4 over a loopback socket in C++ (include/suruga over
+    the C ABI), linked against the in-tree library (a measuring tool, not the
+    product)."""
+    lib = build_library()
+    deps = [LOOPBACK_SRC, ROOT / "include" / "suruga" / "cipher.hpp", ROOT / "include" / "suruga" / "tls.hpp",
+            ROOT / "include" / "suruga_gpu.h", lib]
+    if force or _stale(LOOPBACK_BIN, deps):
+        tmp = LOOPBACK_BIN.with_suffix(f".tmp{os.getpid()}")
+        _run(["g++", "-std=c++17", "-O2", "-Wall", "-Wextra", "-pthread", "-o", str(tmp), str(LOOPBACK_SRC),
+              f"-L{lib.parent}", "-lsuruga_gpu", "-Wl,-rpath,$ORIGIN/../suruga_amd"])
+        os.replace(tmp, LOOPBACK_BIN)
+    return LOOPBACK_BIN
+
+
 def build_all(force: bool = False) -> None:
     build_library(force)
     build_oracle(force)
     build_ossl(force)
     build_cpp_tests(force)
+    build_loopback_cpp(force)
 
 
 if __name__ == "__main__":

@@ -35,6 +35,7 @@ EXPORTS = [
     "sg_fill_records", "sg_compare_records",
     "sg_last_error", "sg_build_info", "sg_source_hash", "sg_set_timing", "sg_timing_read", "sg_set_lockstep", "sg_set_packed",
     "sg_wire_bound", "sg_write_records", "sg_read_records", "sg_parse_records", "sg_record_timing",
+    "sg_host_register", "sg_host_unregister",
     "sg_sha256", "sg_hmac_sha256", "sg_prf_new", "sg_prf_get_bytes", "sg_prf_free",
     "sg_derive_keys", "sg_finished_verify_data",
 ]
@@ -169,6 +170,10 @@ def _declare(lib: C.CDLL) -> None:
     lib.sg_read_records.restype = C.c_int
     lib.sg_read_records.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t,
                                     C.c_void_p, C.c_void_p, C.c_size_t, C.POINTER(SgReadResult)]
+    lib.sg_host_register.restype = C.c_int
+    lib.sg_host_register.argtypes = [C.c_void_p, C.c_size_t]
+    lib.sg_host_unregister.restype = C.c_int
+    lib.sg_host_unregister.argtypes = [C.c_void_p]
     lib.sg_parse_records.restype = C.c_int
     lib.sg_parse_records.argtypes = [C.c_void_p, C.c_size_t, C.c_size_t, C.POINTER(SgWireRecord),
                                      C.POINTER(C.c_size_t), C.POINTER(C.c_int32)]

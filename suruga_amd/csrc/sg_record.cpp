@@ -244,6 +244,34 @@ inline void put_be64(uint8_t* p, uint64_t v) {
     for (int i = 0; i < 8; ++i) p[i] = (uint8_t)(v >> (56 - 8 * i));
 }
 
+// Caller buffers registered with sg_host_register (page-locked, device-visible
+// host memory).  When a call's source and destination both lie in registered
+// ranges, the record bytes move by DMA straight between them and the device
+// (no framing copy through the library's pinned staging): sg_write_records
+// copies the plaintext in one contiguous H2D per chunk and the sealed
+// fragments out with one strided D2H into their wire slots (the 5-byte
+// headers are written by the host); sg_read_records copies the fragments in
+// with one strided H2D and the plaintext out contiguously.
+std::mutex g_reg_mu;
+std::vector<std::pair<uintptr_t, uintptr_t>> g_reg;  // [lo, hi)
+bool registered(const void* p, size_t n) {
+    if (!p || !n) return false;
+    const uintptr_t lo = (uintptr_t)p, hi = lo + n;
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    for (const auto& r : g_reg)
+        if (lo >= r.first && hi <= r.second) return true;
+    return false;
+}
+
+// SG_ZERO_COPY=0 in the environment turns the registered-buffer path off (A/B)
+bool zero_copy_enabled() {
+    static const bool on = [] {
+        const char* e = std::getenv("SG_ZERO_COPY");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 }  // namespace
 }  // namespace sg
 
@@ -254,6 +282,27 @@ extern "C" {
 size_t sg_wire_bound(size_t len) {
     const size_t recs = (len + SG_RECORD_MAX_LEN - 1) / SG_RECORD_MAX_LEN;
     return len + recs * (SG_HEADER_LEN + SG_MAC_LEN);
+}
+
+int sg_host_register(void* p, size_t len) {
+    if (!p || !len) return fail(SG_E_ARG, "NULL or empty range%s");
+    const hipError_t e = hipHostRegister(p, len, hipHostRegisterPortable);
+    if (e != hipSuccess) return sg::hip_fail(e, "hipHostRegister");
+    std::lock_guard<std::mutex> lk(sg::g_reg_mu);
+    sg::g_reg.emplace_back((uintptr_t)p, (uintptr_t)p + len);
+    return SG_OK;
+}
+
+int sg_host_unregister(void* p) {
+    {
+        std::lock_guard<std::mutex> lk(sg::g_reg_mu);
+        auto it = std::find_if(sg::g_reg.begin(), sg::g_reg.end(),
+                               [&](const std::pair<uintptr_t, uintptr_t>& r) { return r.first == (uintptr_t)p; });
+        if (it == sg::g_reg.end()) return fail(SG_E_ARG, "range was not registered with sg_host_register%s");
+        sg::g_reg.erase(it);
+    }
+    const hipError_t e = hipHostUnregister(p);
+    return e == hipSuccess ? SG_OK : sg::hip_fail(e, "hipHostUnregister");
 }
 
 int sg_record_timing(double* h2d_ms, double* kernel_ms, double* d2h_ms, double* host_ms) {
@@ -281,25 +330,36 @@ int64_t sg_write_records(sg_ctx* c, uint64_t seq0, uint8_t content_type, uint8_t
     if (rc != SG_OK) return rc;
     SlotReset slot_reset(rs);
     size_t wpos = 0;
-
-    // frame a drained slot's records into the wire (tls.rs:126-130)
     // every record but the last is full, so record r starts at r * kWireRec
     constexpr size_t kWireRec = SG_HEADER_LEN + SG_RECORD_MAX_LEN + SG_MAC_LEN;
+    const size_t wire_need = (size_t)(nrec - 1) * kWireRec + SG_HEADER_LEN +
+                             (size_t)(len - (nrec - 1) * SG_RECORD_MAX_LEN) + SG_MAC_LEN;
+    // registered caller buffers: DMA straight between them and the device
+    const bool zc = zero_copy_enabled() && registered(data, len) && registered(wire, wire_need);
+    auto rec_len = [&](uint64_t r) { return (uint32_t)std::min<uint64_t>(SG_RECORD_MAX_LEN, len - r * SG_RECORD_MAX_LEN); };
+
+    // frame a drained slot's records into the wire (tls.rs:126-130): the
+    // headers, and (staged path) the fragments from the pinned staging
     auto emit = [&](RecordStaging::Slot& s) {
         const double t0 = now_ms();
-        copy_run(s.nrec, [&](uint32_t i) {
-            const uint64_t r = s.first + i;
-            const uint32_t n = (uint32_t)std::min<uint64_t>(SG_RECORD_MAX_LEN, len - r * SG_RECORD_MAX_LEN);
+        auto header = [&](uint64_t r) {
             uint8_t* h = wire + r * kWireRec;
             h[0] = content_type;
             h[1] = ver_major;
             h[2] = ver_minor;
-            put_be16(h + 3, n + SG_MAC_LEN);
-            std::memcpy(h + SG_HEADER_LEN, s.h_out + (size_t)i * kSlot, n + SG_MAC_LEN);
-        });
+            put_be16(h + 3, rec_len(r) + SG_MAC_LEN);
+        };
+        if (zc) {
+            for (uint32_t i = 0; i < s.nrec; ++i) header(s.first + i);
+        } else {
+            copy_run(s.nrec, [&](uint32_t i) {
+                const uint64_t r = s.first + i;
+                header(r);
+                std::memcpy(wire + r * kWireRec + SG_HEADER_LEN, s.h_out + (size_t)i * kSlot, rec_len(r) + SG_MAC_LEN);
+            });
+        }
         const uint64_t last = s.first + s.nrec - 1;
-        wpos = last * kWireRec + SG_HEADER_LEN +
-               (size_t)std::min<uint64_t>(SG_RECORD_MAX_LEN, len - last * SG_RECORD_MAX_LEN) + SG_MAC_LEN;
+        wpos = last * kWireRec + SG_HEADER_LEN + (size_t)rec_len(last) + SG_MAC_LEN;
         t_host += now_ms() - t0;
     };
 
@@ -314,18 +374,29 @@ int64_t sg_write_records(sg_ctx* c, uint64_t seq0, uint8_t content_type, uint8_t
         if (next < nrec) {
             const uint32_t k = (uint32_t)std::min<uint64_t>(kChunk, nrec - next);
             const double t0 = now_ms();
-            copy_run(k, [&](uint32_t i) {
-                const uint64_t r = next + i;
-                const uint32_t n = (uint32_t)std::min<uint64_t>(SG_RECORD_MAX_LEN, len - r * SG_RECORD_MAX_LEN);
-                std::memcpy(s.h_in + (size_t)i * kSlot, data + r * SG_RECORD_MAX_LEN, n);
-                s.h_len[i] = n;
-            });
+            // zero-copy: the chunk's plaintext is contiguous in the caller's buffer
+            // (in_stride 2^14); staged: each record in its 16-byte aligned slot
+            if (zc) {
+                for (uint32_t i = 0; i < k; ++i) s.h_len[i] = rec_len(next + i);
+            } else {
+                copy_run(k, [&](uint32_t i) {
+                    const uint64_t r = next + i;
+                    std::memcpy(s.h_in + (size_t)i * kSlot, data + r * SG_RECORD_MAX_LEN, rec_len(r));
+                    s.h_len[i] = rec_len(r);
+                });
+            }
             bool same = true;  // every record of the chunk has the same length
             for (uint32_t i = 1; i < k; ++i) same = same && s.h_len[i] == s.h_len[0];
             t_host += now_ms() - t0;
+            const size_t in_stride = zc ? SG_RECORD_MAX_LEN : kSlot;
             SG_HIP(hipEventRecord(s.ev[0], s.st));
-            SG_HIP(hipMemcpyAsync(s.d_in, s.h_in, (size_t)k * kSlot, hipMemcpyHostToDevice, s.st));
-            SG_HIP(hipMemcpyAsync(s.d_len, s.h_len, k * 4u, hipMemcpyHostToDevice, s.st));
+            if (zc) {
+                const size_t bytes = (size_t)(k - 1) * SG_RECORD_MAX_LEN + s.h_len[k - 1];
+                SG_HIP(hipMemcpyAsync(s.d_in, data + next * SG_RECORD_MAX_LEN, bytes, hipMemcpyHostToDevice, s.st));
+            } else {
+                SG_HIP(hipMemcpyAsync(s.d_in, s.h_in, (size_t)k * kSlot, hipMemcpyHostToDevice, s.st));
+            }
+            if (!same) SG_HIP(hipMemcpyAsync(s.d_len, s.h_len, k * 4u, hipMemcpyHostToDevice, s.st));
             SG_HIP(hipEventRecord(s.ev[1], s.st));
             sg_batch b;
             std::memset(&b, 0, sizeof b);
@@ -338,7 +409,7 @@ int64_t sg_write_records(sg_ctx* c, uint64_t seq0, uint8_t content_type, uint8_t
             b.ver_major = ver_major;
             b.ver_minor = ver_minor;
             b.in = s.d_in;
-            b.in_stride = kSlot;
+            b.in_stride = in_stride;
             b.out = s.d_out;
             b.out_stride = kSlot;
             // a uniform chunk is a direct launch; a ragged one (the tail) is bucketed
@@ -350,7 +421,20 @@ int64_t sg_write_records(sg_ctx* c, uint64_t seq0, uint8_t content_type, uint8_t
             b.workspace_size = sg_workspace_size(kChunk);
             if ((rc = sg_seal_batch(&b)) != SG_OK) return rc;
             SG_HIP(hipEventRecord(s.ev[2], s.st));
-            SG_HIP(hipMemcpyAsync(s.h_out, s.d_out, (size_t)k * kSlot, hipMemcpyDeviceToHost, s.st));
+            if (zc) {
+                // fragments (ct || tag) into their wire slots: full records with one
+                // strided copy (pitch kWireRec), the partial last record alone
+                const uint32_t full = s.h_len[k - 1] == SG_RECORD_MAX_LEN ? k : k - 1;
+                uint8_t* w0 = wire + next * kWireRec + SG_HEADER_LEN;
+                if (full)
+                    SG_HIP(hipMemcpy2DAsync(w0, kWireRec, s.d_out, kSlot, SG_RECORD_MAX_LEN + SG_MAC_LEN, full,
+                                            hipMemcpyDeviceToHost, s.st));
+                if (full < k)
+                    SG_HIP(hipMemcpyAsync(w0 + (size_t)full * kWireRec, s.d_out + (size_t)full * kSlot,
+                                          s.h_len[k - 1] + SG_MAC_LEN, hipMemcpyDeviceToHost, s.st));
+            } else {
+                SG_HIP(hipMemcpyAsync(s.h_out, s.d_out, (size_t)k * kSlot, hipMemcpyDeviceToHost, s.st));
+            }
             SG_HIP(hipEventRecord(s.ev[3], s.st));
             s.nrec = k;
             s.first = next;
@@ -394,10 +478,24 @@ int sg_read_records(sg_ctx* c, uint64_t seq0, const uint8_t* wire, size_t wire_l
     const uint64_t nrec = recs.size();
     uint64_t next = 0, good = 0, opos = 0, consumed = 0;
     int32_t error = SG_OK;
+    // registered caller buffers: the fragments come in by DMA from the wire and
+    // the plaintext leaves by DMA into `out` at its final offset (prefix sum of
+    // the plaintext lengths, as if every record opens)
+    const bool zc = zero_copy_enabled() && registered(wire, wire_len) && registered(out, need);
+    std::vector<uint64_t> pre;  // zc: plaintext offset of every record
+    if (zc) {
+        pre.resize(nrec + 1);
+        pre[0] = 0;
+        for (uint64_t i = 0; i < nrec; ++i) pre[i + 1] = pre[i] + recs[i].flen - SG_MAC_LEN;
+    }
     std::vector<uint64_t> dst_off(kChunk);
-    auto collect = [&](RecordStaging::Slot& s) {
+    std::vector<uint8_t> chunk_zc(2, 0);  // per slot: the chunk went the zero-copy way
+    auto collect = [&](RecordStaging::Slot& s, bool szc) {
         const double t0 = now_ms();
-        if (error != SG_OK) return;
+        if (error != SG_OK) {  // stopped earlier: nothing of this chunk is delivered
+            if (szc) std::memset(out + pre[s.first], 0, pre[s.first + s.nrec] - pre[s.first]);
+            return;
+        }
         // the records up to the first failing one are delivered (tls.rs:268: the
         // reader stops at its first Err); their output offsets are a prefix sum
         uint32_t ok = 0;
@@ -411,14 +509,25 @@ int sg_read_records(sg_ctx* c, uint64_t seq0, const uint8_t* wire, size_t wire_l
             opos += R.flen - SG_MAC_LEN;
             consumed += SG_HEADER_LEN + R.flen;
         }
-        copy_run(ok, [&](uint32_t i) {
-            const uint64_t r = s.first + i;
-            const Rec& R = recs[r];
-            const uint32_t n = R.flen - SG_MAC_LEN;
-            std::memcpy(out + dst_off[i], s.h_out + (size_t)i * kSlot, n);
-            if (types) types[r] = R.type;
-            if (frag_lens) frag_lens[r] = n;
-        });
+        if (szc) {
+            // the plaintext is in place already; from a failed record on, the
+            // DMA'd bytes are cleared (the reference releases none of them)
+            if (ok < s.nrec) std::memset(out + pre[s.first + ok], 0, pre[s.first + s.nrec] - pre[s.first + ok]);
+            for (uint32_t i = 0; i < ok; ++i) {
+                const uint64_t r = s.first + i;
+                if (types) types[r] = recs[r].type;
+                if (frag_lens) frag_lens[r] = recs[r].flen - SG_MAC_LEN;
+            }
+        } else {
+            copy_run(ok, [&](uint32_t i) {
+                const uint64_t r = s.first + i;
+                const Rec& R = recs[r];
+                const uint32_t n = R.flen - SG_MAC_LEN;
+                std::memcpy(out + dst_off[i], s.h_out + (size_t)i * kSlot, n);
+                if (types) types[r] = R.type;
+                if (frag_lens) frag_lens[r] = n;
+            });
+        }
         good += ok;
         t_host += now_ms() - t0;
     };
@@ -428,62 +537,103 @@ int sg_read_records(sg_ctx* c, uint64_t seq0, const uint8_t* wire, size_t wire_l
         RecordStaging::Slot& s = rs->slot[cur];
         if (s.busy) {
             if ((rc = drain(s)) != SG_OK) return rc;
-            collect(s);
+            collect(s, chunk_zc[cur] != 0);
         }
         if (next < nrec && error == SG_OK) {
             const uint32_t k = (uint32_t)std::min<uint64_t>(kChunk, nrec - next);
             const double t0 = now_ms();
-            bool same = true;
-            for (uint32_t i = 0; i < k; ++i) same = same && recs[next + i].flen == recs[next].flen;
-            copy_run(k, [&](uint32_t i) {
+            const Rec& R0 = recs[next];
+            bool same = true, tls = true, dense = true;
+            for (uint32_t i = 0; i < k; ++i) {
                 const Rec& R = recs[next + i];
-                const uint64_t seq = seq0 + next + i;
-                std::memcpy(s.h_in + (size_t)i * kSlot, wire + R.off, R.flen);
-                s.h_len[i] = R.flen;
-                // nonce = be64(seq) (tls.rs:250); AD = seq || type || major || minor ||
-                // be16(len - 16) (tls.rs:252-265).  Layout: nonces[kChunk][8], ads[kChunk][13]
-                put_be64(s.h_meta + 8u * i, seq);
-                uint8_t* m = s.h_meta + 8u * kChunk + 13u * i;
-                put_be64(m, seq);
-                m[8] = R.type;
-                m[9] = R.major;
-                m[10] = R.minor;
-                put_be16(m + 11, R.flen - SG_MAC_LEN);
-            });
+                same = same && R.flen == R0.flen;
+                tls = tls && R.type == R0.type && R.major == R0.major && R.minor == R0.minor;
+                dense = dense && R.off == R0.off + (size_t)i * (SG_HEADER_LEN + R0.flen);
+            }
+            // zero-copy for chunks of equal, back-to-back records (a stream of
+            // full records); any other chunk goes through the staging
+            const bool czc = zc && same && dense;
+            chunk_zc[cur] = czc ? 1 : 0;
+            // TLS mode (nonce and AD built on the device, tls.rs:250-265) when the
+            // chunk's records share type and version; else explicit nonce / AD
+            if (!czc) {
+                copy_run(k, [&](uint32_t i) {
+                    const Rec& R = recs[next + i];
+                    std::memcpy(s.h_in + (size_t)i * kSlot, wire + R.off, R.flen);
+                    s.h_len[i] = R.flen;
+                });
+            }
+            if (!tls) {
+                for (uint32_t i = 0; i < k; ++i) {
+                    const Rec& R = recs[next + i];
+                    const uint64_t seq = seq0 + next + i;
+                    // nonce = be64(seq) (tls.rs:250); AD = seq || type || major || minor ||
+                    // be16(len - 16) (tls.rs:252-265).  Layout: nonces[kChunk][8], ads[kChunk][13]
+                    put_be64(s.h_meta + 8u * i, seq);
+                    uint8_t* m = s.h_meta + 8u * kChunk + 13u * i;
+                    put_be64(m, seq);
+                    m[8] = R.type;
+                    m[9] = R.major;
+                    m[10] = R.minor;
+                    put_be16(m + 11, R.flen - SG_MAC_LEN);
+                }
+            }
             t_host += now_ms() - t0;
             SG_HIP(hipEventRecord(s.ev[0], s.st));
-            SG_HIP(hipMemcpyAsync(s.d_in, s.h_in, (size_t)k * kSlot, hipMemcpyHostToDevice, s.st));
-            SG_HIP(hipMemcpyAsync(s.d_len, s.h_len, k * 4u, hipMemcpyHostToDevice, s.st));
-            SG_HIP(hipMemcpyAsync(s.d_meta, s.h_meta, 8u * k, hipMemcpyHostToDevice, s.st));
-            SG_HIP(hipMemcpyAsync(s.d_meta + 8u * kChunk, s.h_meta + 8u * kChunk, 13u * k, hipMemcpyHostToDevice,
-                                  s.st));
+            if (czc) {  // the fragments, one strided copy out of the wire
+                SG_HIP(hipMemcpy2DAsync(s.d_in, kSlot, wire + R0.off, SG_HEADER_LEN + R0.flen, R0.flen, k,
+                                        hipMemcpyHostToDevice, s.st));
+            } else {
+                SG_HIP(hipMemcpyAsync(s.d_in, s.h_in, (size_t)k * kSlot, hipMemcpyHostToDevice, s.st));
+                if (!same) SG_HIP(hipMemcpyAsync(s.d_len, s.h_len, k * 4u, hipMemcpyHostToDevice, s.st));
+            }
+            if (!tls) {
+                SG_HIP(hipMemcpyAsync(s.d_meta, s.h_meta, 8u * k, hipMemcpyHostToDevice, s.st));
+                SG_HIP(hipMemcpyAsync(s.d_meta + 8u * kChunk, s.h_meta + 8u * kChunk, 13u * k, hipMemcpyHostToDevice,
+                                      s.st));
+            }
             SG_HIP(hipEventRecord(s.ev[1], s.st));
             sg_batch b;
             std::memset(&b, 0, sizeof b);
             b.count = k;
             b.keys = c->d_key;
             b.num_keys = 1;
-            b.nonces = s.d_meta;
-            b.ads = s.d_meta + 8u * kChunk;
-            b.ad_len = 13;
-            b.ad_stride = 13;
+            if (tls) {
+                b.flags = SG_BATCH_TLS;
+                b.seq0 = seq0 + next;
+                b.content_type = R0.type;
+                b.ver_major = R0.major;
+                b.ver_minor = R0.minor;
+            } else {
+                b.nonces = s.d_meta;
+                b.ads = s.d_meta + 8u * kChunk;
+                b.ad_len = 13;
+                b.ad_stride = 13;
+            }
             b.in = s.d_in;
             b.in_stride = kSlot;
             b.out = s.d_out;
-            b.out_stride = kSlot;
+            // zero-copy: plaintext back to back, as it lands in `out`
+            b.out_stride = czc ? (size_t)(R0.flen - SG_MAC_LEN) : kSlot;
             b.len = same ? nullptr : s.d_len;
-            b.uniform_len = same ? recs[next].flen : 0u;
+            b.uniform_len = same ? R0.flen : 0u;
             b.max_len = SG_ENC_RECORD_MAX_LEN;
             b.status = s.d_status;
             b.stream = s.st;
             b.workspace = s.d_ws;
             b.workspace_size = sg_workspace_size(kChunk);
-            // the reader delivers nothing from a failed record (it stops there):
-            // no device scrub of failed records' output
-            b.flags = SG_BATCH_KEEP_FAILED;
+            // staged: the reader delivers nothing from a failed record (it stops
+            // there), so no device scrub of failed records' output; zero-copy: the
+            // output goes to the caller's memory by DMA, so failed records are
+            // scrubbed on the device first
+            if (!czc) b.flags |= SG_BATCH_KEEP_FAILED;
             if ((rc = sg_open_batch(&b)) != SG_OK) return rc;
             SG_HIP(hipEventRecord(s.ev[2], s.st));
-            SG_HIP(hipMemcpyAsync(s.h_out, s.d_out, (size_t)k * kSlot, hipMemcpyDeviceToHost, s.st));
+            if (czc) {
+                SG_HIP(hipMemcpyAsync(out + pre[next], s.d_out, pre[next + k] - pre[next], hipMemcpyDeviceToHost, s.st));
+            } else {
+                SG_HIP(hipMemcpyAsync(s.h_out, s.d_out, (size_t)k * kSlot, hipMemcpyDeviceToHost, s.st));
+            }
             SG_HIP(hipMemcpyAsync(s.h_status, s.d_status, k, hipMemcpyDeviceToHost, s.st));
             SG_HIP(hipEventRecord(s.ev[3], s.st));
             s.nrec = k;

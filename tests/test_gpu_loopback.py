@@ -51,3 +51,23 @@ def test_record_path_both_directions_bit_exact(gpu):
     r = RP.one(32 << 20, 8 << 20, 0)
     assert r["correct"], r
     assert r["records"] == (32 << 20) // REC
+
+
+@pytest.mark.parametrize("registered", [False, True])
+def test_cpp_loopback_every_byte(gpu, registered):
+    """tools/loopback_cpp (C4 in C++ over include/suruga, no Python on the data
+    path): 64 MiB over a loopback socket, staged and zero-copy (registered
+    buffers); the harness compares every delivered byte with the stream."""
+    import json
+    import subprocess
+
+    from suruga_amd import _build
+
+    exe = _build.build_loopback_cpp()
+    args = [str(exe), "--bytes", str(64 << 20), "--chunk", str(8 << 20), "--block", str(8 << 20)]
+    p = subprocess.run(args + (["--registered"] if registered else []), capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stdout + p.stderr
+    j = json.loads(p.stdout.strip().splitlines()[-1])
+    assert j["correct"] and j["registered"] is registered
+    assert j["reader"]["bytes"] == 64 << 20 and j["reader"]["mismatched_bytes"] == 0
+    assert j["writer"]["records"] == (64 << 20) // REC == j["reader"]["records"]

@@ -289,3 +289,69 @@ def test_parse_records_header_checks_cpu():
     assert parse(rec(23, RECORD_MAX_LEN + 17))[1] == N.SG_E_RECORD_OVERFLOW  # decrypted > 2^14 (:269-272)
     assert parse(rec(23, RECORD_MAX_LEN + 16)) == ([(5, RECORD_MAX_LEN + 16, 23, 3, 3)], N.SG_OK)
     assert parse(b"") == ([], N.SG_OK)
+
+
+@pytest.mark.gpu
+def test_gpu_zero_copy_record_path(gpu, oracle):
+    """sg_host_register'ed caller buffers: sg_write_records
+    DMAs the plaintext straight from `data` and the sealed fragments straight
+    into their wire slots, sg_read_records the fragments straight from the wire
+    and the plaintext straight into `out`.  The wire equals the staged path's
+    (and the oracle's) byte for byte, the read-back equals the input; with a
+    corrupted record the records before it are delivered and `out` holds
+    nothing of it or of any record after it."""
+    import ctypes as C
+
+    import numpy as np
+
+    from suruga_amd import ChaCha20Poly1305
+    from suruga_amd import _native as N
+
+    lib = N.load()
+    key = bytes(range(7, 39))
+    total = 600 * RECORD_MAX_LEN + 4321  # three chunks of 256 records and a ragged tail
+    data = np.frombuffer(oracle.fill_record(0x5A, 3, total), dtype=np.uint8).copy()
+    enc, dec = ChaCha20Poly1305().new_encryptor(key), ChaCha20Poly1305().new_decryptor(key)
+    cap = lib.sg_wire_bound(total)
+    staged = np.zeros(cap, dtype=np.uint8)
+    wl = C.c_size_t(0)
+    nrec = N.check(lib.sg_write_records(enc._ptr, 5, 23, 3, 3, data.ctypes.data, total, staged.ctypes.data, cap,
+                                        C.byref(wl)))
+    wlen = wl.value
+    wire = np.zeros(cap, dtype=np.uint8)
+    out = np.full(total, 0xEE, dtype=np.uint8)
+    for a in (data, wire, out):
+        N.check(lib.sg_host_register(a.ctypes.data, a.nbytes))
+    try:
+        wl2 = C.c_size_t(0)
+        assert N.check(lib.sg_write_records(enc._ptr, 5, 23, 3, 3, data.ctypes.data, total, wire.ctypes.data, cap,
+                                            C.byref(wl2))) == nrec
+        assert wl2.value == wlen and np.array_equal(wire[:wlen], staged[:wlen])
+        # spot-check against the oracle: first, a middle and the last record
+        rec = 5 + RECORD_MAX_LEN + 16
+        for r in (0, 300, nrec - 1):
+            n = min(RECORD_MAX_LEN, total - r * RECORD_MAX_LEN)
+            pt = data[r * RECORD_MAX_LEN:r * RECORD_MAX_LEN + n].tobytes()
+            exp = oracle.seal(key, struct.pack(">Q", 5 + r), pt, oracle.tls_ad(5 + r, n))
+            assert wire[r * rec + 5:r * rec + 5 + n + 16].tobytes() == exp, r
+        res = N.SgReadResult()
+        N.check(lib.sg_read_records(dec._ptr, 5, wire.ctypes.data, wlen, out.ctypes.data, total, None, None, 1 << 20,
+                                    C.byref(res)))
+        assert (res.records, res.consumed, res.out_len, res.error) == (nrec, wlen, total, N.SG_OK)
+        assert np.array_equal(out, data)
+        # a corrupted record in the second chunk: records before it delivered, nothing after
+        bad = 300
+        wire[bad * rec + 5 + 1000] ^= 0x10
+        out[:] = 0xEE
+        N.check(lib.sg_read_records(dec._ptr, 5, wire.ctypes.data, wlen, out.ctypes.data, total, None, None, 1 << 20,
+                                    C.byref(res)))
+        assert (res.records, res.out_len, res.error) == (bad, bad * RECORD_MAX_LEN, N.SG_E_BAD_MAC)
+        assert np.array_equal(out[:bad * RECORD_MAX_LEN], data[:bad * RECORD_MAX_LEN])
+        leaked = [r for r in range(bad, nrec)
+                  if r * RECORD_MAX_LEN < total and
+                  np.array_equal(out[r * RECORD_MAX_LEN:min(total, (r + 1) * RECORD_MAX_LEN)],
+                                 data[r * RECORD_MAX_LEN:min(total, (r + 1) * RECORD_MAX_LEN)])]
+        assert leaked == [], f"plaintext of undelivered records {leaked[:5]} in out"
+    finally:
+        for a in (data, wire, out):
+            N.check(lib.sg_host_unregister(a.ctypes.data))

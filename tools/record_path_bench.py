@@ -31,7 +31,7 @@ sys.path.insert(0, str(ROOT))
 KEY = bytes(range(32))
 
 
-def one(total: int, call: int, device: int) -> dict:
+def one(total: int, call: int, device: int, registered: bool = False) -> dict:
     import numpy as np
 
     from suruga_amd import ChaCha20Poly1305
@@ -43,6 +43,9 @@ def one(total: int, call: int, device: int) -> dict:
     back = np.empty(total, dtype=np.uint8)
     aead = ChaCha20Poly1305(device)
     enc, dec = aead.new_encryptor(KEY), aead.new_decryptor(KEY)
+    if registered:  # the zero-copy path: DMA straight between these buffers and the device
+        for a in (data, wire, back):
+            N.check(lib.sg_host_register(a.ctypes.data, a.nbytes))
 
     def timing(acc):
         v = [C.c_double() for _ in range(4)]
@@ -91,11 +94,14 @@ def one(total: int, call: int, device: int) -> dict:
     rrec, olen = read_all(wlen, racc)
     tr = time.perf_counter() - t0
     ok = rrec == nrec and olen == total and bool(np.array_equal(back, data))
+    if registered:
+        for a in (data, wire, back):
+            N.check(lib.sg_host_unregister(a.ctypes.data))
     gib = total / 2**30
     per = lambda acc: {k + "_ms_per_gib": round(v / gib, 2) for k, v in acc.items()}  # noqa: E731
     return {"write_gibs": round(gib / tw, 3), "read_gibs": round(gib / tr, 3), "write_ms": round(tw * 1e3, 1),
             "read_ms": round(tr * 1e3, 1), "records": nrec, "correct": ok, "write_split": per(wacc),
-            "read_split": per(racc)}
+            "read_split": per(racc), "registered": registered}
 
 
 def main():
@@ -104,6 +110,8 @@ def main():
     ap.add_argument("--call-bytes", type=int, default=64 << 20, help="application bytes per write call")
     ap.add_argument("--threads", default="1,4,8", help="SG_COPY_THREADS values (one child process each)")
     ap.add_argument("--device", type=int, default=0)
+    ap.add_argument("--registered", default="0", help="0, 1 or 0,1: caller buffers registered with sg_host_register "
+                    "(the zero-copy path)")
     ap.add_argument("--json-out")
     ap.add_argument("--child", action="store_true")
     ap.add_argument("--watchdog", type=float, default=0, help="dump every thread's stack and exit after this many s")
@@ -113,22 +121,24 @@ def main():
 
         faulthandler.dump_traceback_later(a.watchdog, exit=True)
     if a.child:
-        print(json.dumps(one(a.bytes, a.call_bytes, a.device)))
+        print(json.dumps(one(a.bytes, a.call_bytes, a.device, a.registered == "1")))
         return
     runs = {}
-    for t in [int(x) for x in a.threads.split(",")]:
-        env = dict(os.environ, SG_COPY_THREADS=str(t))
-        p = subprocess.run([sys.executable, __file__, "--child", "--bytes", str(a.bytes), "--call-bytes",
-                            str(a.call_bytes), "--device", str(a.device)], env=env, capture_output=True, text=True,
-                           timeout=600)
-        if p.returncode != 0:
-            raise SystemExit(f"threads={t} failed:\n{p.stdout}\n{p.stderr}")
-        runs[str(t)] = json.loads(p.stdout.strip().splitlines()[-1])
+    for reg in a.registered.split(","):
+        for t in [int(x) for x in a.threads.split(",")]:
+            env = dict(os.environ, SG_COPY_THREADS=str(t))
+            p = subprocess.run([sys.executable, __file__, "--child", "--bytes", str(a.bytes), "--call-bytes",
+                                str(a.call_bytes), "--device", str(a.device), "--registered", reg], env=env,
+                               capture_output=True, text=True, timeout=600)
+            if p.returncode != 0:
+                raise SystemExit(f"threads={t} registered={reg} failed:\n{p.stdout}\n{p.stderr}")
+            runs[str(t) + ("+registered" if reg == "1" else "")] = json.loads(p.stdout.strip().splitlines()[-1])
     from suruga_amd import _native as N
 
     lib = N.load()
     out = {"config": f"C4 host side: {a.bytes} B application data, {a.call_bytes} B per sg_write_records call, "
-                     "pageable host buffers, one direction at a time, wall clock around the calls",
+                     "pageable host buffers (\"+registered\": registered with sg_host_register, the zero-copy path), "
+                     "one direction at a time, wall clock around the calls",
            "kernels": lib.sg_build_info().decode(), "library": N.loaded_info(),
            "host_cpus": len(os.sched_getaffinity(0)), "by_copy_threads": runs,
            "correct": all(r["correct"] for r in runs.values())}
