@@ -192,6 +192,14 @@ hipError_t launch_pack(const KParams& p, bool open, const uint32_t* list, const 
 const char* pack_kernel_config();
 // zero the output of every record whose open status is 1 (wrong mac)
 hipError_t launch_scrub(const KParams& p, hipStream_t s);
+// record-layer framing in HBM (sg_record.cpp zero-copy path): build the wire
+// image of `count` records (pitch = 5 + frag; the last record's fragment
+// last_frag) from aligned fragment slots, or take the fragments of a wire
+// image of equal records back into slots
+hipError_t launch_frame(const uint8_t* src, uint32_t src_stride, uint8_t* dst, uint32_t pitch, uint32_t count,
+                        uint32_t frag, uint32_t last_frag, uint32_t hdr, hipStream_t s);
+hipError_t launch_unframe(const uint8_t* src, uint32_t pitch, uint8_t* dst, uint32_t dst_stride, uint32_t count,
+                          uint32_t frag, hipStream_t s);
 hipError_t launch_fill(uint8_t* buf, uint64_t stride, uint32_t len, uint32_t count, uint64_t seed,
                        uint64_t j0, hipStream_t s);
 hipError_t launch_compare(const uint8_t* a, uint64_t sa, const uint8_t* b, uint64_t sb, uint32_t len,

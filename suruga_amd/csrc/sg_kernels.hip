@@ -31,6 +31,7 @@
 // All Poly1305 arithmetic is exact mod p = 2^130 - 5, so the tag equals the
 // reference's sequential Horner result bit for bit.
 #include "sg_internal.h"
+#include "../../include/suruga_gpu.h"  // SG_HEADER_LEN (record-layer framing kernels)
 
 #include <mutex>
 #include <vector>
@@ -670,6 +671,86 @@ __global__ __launch_bounds__(256) void sg_compare_kernel(const uint8_t* a, uint6
     }
 }
 
+// ---------------------------------------------------------------------------
+// Record-layer framing on the device (sg_record.cpp, registered caller
+// buffers): the wire image of a chunk is built / taken apart in HBM so that
+// the host link moves one contiguous run each way (a strided host-side copy
+// at the wire's 16,405-byte pitch measured ~1.3 s per GiB).  Wire record r
+// sits at r * pitch: the 5-byte header (tls.rs:126-130) and its fragment.
+// One thread per 4-byte word of the destination; source words are read
+// aligned and funnel-shifted (v_alignbyte) into place.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t ld_u32_unaligned(const uint8_t* p) {
+    const uintptr_t a = (uintptr_t)p;
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
+    return __builtin_amdgcn_alignbyte(q[1], q[0], (uint32_t)(a & 3u));
+}
+
+// dst[0, image) <- headers and fragments; fragment r = src + r * src_stride,
+// frag bytes (last: last_frag); hdr = type | major << 8 | minor << 16.
+// rdiv: ceil(2^40 / pitch) (r = b * rdiv >> 40 is exact for b < 2^40 / pitch;
+// launch_frame caps the image at 2^24 bytes, a chunk is ~4.2 MB).
+__global__ __launch_bounds__(256) void sg_frame_kernel(const uint8_t* __restrict__ src, uint32_t src_stride,
+                                                       uint8_t* __restrict__ dst, uint32_t pitch, uint64_t rdiv,
+                                                       uint32_t count, uint32_t frag, uint32_t last_frag,
+                                                       uint32_t hdr) {
+    const uint32_t image = (count - 1u) * pitch + SG_HEADER_LEN + last_frag;
+    const uint32_t nw = (image + 3u) >> 2;
+    for (uint32_t w = blockIdx.x * 256u + threadIdx.x; w < nw; w += gridDim.x * 256u) {
+        const uint32_t b0 = 4u * w;
+        const uint32_t r = (uint32_t)(((uint64_t)b0 * rdiv) >> 40);
+        const uint32_t o = b0 - r * pitch;  // offset in record r's wire slot
+        const uint32_t fl = r + 1u == count ? last_frag : frag;
+        if (o >= SG_HEADER_LEN && o + 4u <= SG_HEADER_LEN + fl) {  // inside one fragment
+            reinterpret_cast<uint32_t*>(dst)[w] = ld_u32_unaligned(src + (uint64_t)r * src_stride + (o - SG_HEADER_LEN));
+            continue;
+        }
+        uint32_t v = 0u;
+        for (uint32_t k = 0; k < 4u; ++k) {  // header bytes and record boundaries
+            const uint32_t b = b0 + k;
+            if (b >= image) break;
+            uint32_t rr = r, oo = o + k;
+            if (oo >= pitch) {
+                rr += 1u;
+                oo -= pitch;
+            }
+            const uint32_t f = rr + 1u == count ? last_frag : frag;
+            uint32_t byte;
+            if (oo < SG_HEADER_LEN) {
+                const uint32_t n = f;  // be16 fragment length
+                byte = oo < 3u ? (hdr >> (8u * oo)) & 0xffu : (oo == 3u ? (n >> 8) & 0xffu : n & 0xffu);
+            } else {
+                byte = src[(uint64_t)rr * src_stride + (oo - SG_HEADER_LEN)];
+            }
+            v |= byte << (8u * k);
+        }
+        if (b0 + 4u <= image) {
+            reinterpret_cast<uint32_t*>(dst)[w] = v;
+        } else {
+            for (uint32_t k = 0; b0 + k < image; ++k) dst[b0 + k] = (uint8_t)(v >> (8u * k));
+        }
+    }
+}
+
+// dst + r * dst_stride <- the frag bytes of wire record r (src + r * pitch + 5),
+// count records of one fragment length (src readable 4 bytes past the image).
+__global__ __launch_bounds__(256) void sg_unframe_kernel(const uint8_t* __restrict__ src, uint32_t pitch,
+                                                         uint8_t* __restrict__ dst, uint32_t dst_stride,
+                                                         uint32_t count, uint32_t frag) {
+    const uint32_t wpr = (frag + 3u) >> 2;  // destination words per record
+    const uint32_t total = wpr * count;
+    for (uint32_t g = blockIdx.x * 256u + threadIdx.x; g < total; g += gridDim.x * 256u) {
+        const uint32_t r = g / wpr, w = g - r * wpr;
+        const uint32_t v = ld_u32_unaligned(src + (uint64_t)r * pitch + SG_HEADER_LEN + 4u * w);
+        uint8_t* d = dst + (uint64_t)r * dst_stride + 4u * w;
+        if (4u * w + 4u <= frag) {
+            *reinterpret_cast<uint32_t*>(d) = v;
+        } else {
+            for (uint32_t k = 0; 4u * w + k < frag; ++k) d[k] = (uint8_t)(v >> (8u * k));
+        }
+    }
+}
+
 // Failed opens release no plaintext (chacha20_poly1305.rs:80-93 decrypts
 // unconditionally but returns only Err on a tag mismatch): every record whose
 // status is 1 (wrong mac) gets its output range zeroed after the open
@@ -1022,6 +1103,29 @@ hipError_t launch_aead(const KParams& p, bool open, uint32_t max_n, bool uniform
                        hipEvent_t ev_keyed, hipEvent_t ev_start) {
     return open ? launch_aead_t<true>(p, max_n, uniform, s, over, ev_keyed, ev_start)
                 : launch_aead_t<false>(p, max_n, uniform, s, over, ev_keyed, ev_start);
+}
+
+hipError_t launch_frame(const uint8_t* src, uint32_t src_stride, uint8_t* dst, uint32_t pitch, uint32_t count,
+                        uint32_t frag, uint32_t last_frag, uint32_t hdr, hipStream_t s) {
+    if (count == 0) return hipSuccess;
+    const uint32_t image = (count - 1u) * pitch + SG_HEADER_LEN + last_frag;
+    if (image >= (1u << 24) || (src_stride & 3u) || ((uintptr_t)dst & 3u)) return hipErrorInvalidValue;
+    const uint64_t rdiv = ((1ull << 40) + pitch - 1u) / pitch;
+    uint32_t grid = ((image + 3u) / 4u + 255u) / 256u;
+    grid = grid < 4096u ? grid : 4096u;
+    hipLaunchKernelGGL(sg_frame_kernel, dim3(grid), dim3(256), 0, s, src, src_stride, dst, pitch, rdiv, count, frag,
+                       last_frag, hdr);
+    return hipGetLastError();
+}
+
+hipError_t launch_unframe(const uint8_t* src, uint32_t pitch, uint8_t* dst, uint32_t dst_stride, uint32_t count,
+                          uint32_t frag, hipStream_t s) {
+    if (count == 0) return hipSuccess;
+    if ((dst_stride & 3u) || ((uintptr_t)dst & 3u)) return hipErrorInvalidValue;
+    uint32_t grid = (((frag + 3u) / 4u) * count + 255u) / 256u;
+    grid = grid < 4096u ? grid : 4096u;
+    hipLaunchKernelGGL(sg_unframe_kernel, dim3(grid), dim3(256), 0, s, src, pitch, dst, dst_stride, count, frag);
+    return hipGetLastError();
 }
 
 hipError_t launch_fill(uint8_t* buf, uint64_t stride, uint32_t len, uint32_t count, uint64_t seed,

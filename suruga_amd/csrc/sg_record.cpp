@@ -146,6 +146,7 @@ struct RecordStaging {
         uint8_t *h_in = nullptr, *h_out = nullptr, *h_meta = nullptr, *h_status = nullptr;
         uint32_t* h_len = nullptr;
         uint8_t *d_in = nullptr, *d_out = nullptr, *d_meta = nullptr, *d_status = nullptr;
+        uint8_t* d_wire = nullptr;  // the chunk's wire image (zero-copy path)
         uint32_t* d_len = nullptr;
         void* d_ws = nullptr;
         hipStream_t st = nullptr;
@@ -167,6 +168,7 @@ void record_staging_free(RecordStaging* rs) {
         (void)hipHostFree(s.h_len);
         (void)hipFree(s.d_in);
         (void)hipFree(s.d_out);
+        (void)hipFree(s.d_wire);
         (void)hipFree(s.d_meta);
         (void)hipFree(s.d_status);
         (void)hipFree(s.d_len);
@@ -193,6 +195,7 @@ int staging(sg_ctx* c, RecordStaging** out) {
             SG_HIP(hipHostMalloc((void**)&s.h_len, kChunk * 4u, hipHostMallocDefault));
             SG_HIP(hipMalloc((void**)&s.d_in, bytes));
             SG_HIP(hipMalloc((void**)&s.d_out, bytes));
+            SG_HIP(hipMalloc((void**)&s.d_wire, bytes + 64));
             SG_HIP(hipMalloc((void**)&s.d_meta, (size_t)kChunk * kMetaBytes));
             SG_HIP(hipMalloc((void**)&s.d_status, kChunk));
             SG_HIP(hipMalloc((void**)&s.d_len, kChunk * 4u));
@@ -248,10 +251,10 @@ inline void put_be64(uint8_t* p, uint64_t v) {
 // host memory).  When a call's source and destination both lie in registered
 // ranges, the record bytes move by DMA straight between them and the device
 // (no framing copy through the library's pinned staging): sg_write_records
-// copies the plaintext in one contiguous H2D per chunk and the sealed
-// fragments out with one strided D2H into their wire slots (the 5-byte
-// headers are written by the host); sg_read_records copies the fragments in
-// with one strided H2D and the plaintext out contiguously.
+// copies the plaintext in with one contiguous H2D per chunk, builds the
+// chunk's wire image (headers and fragments) in HBM and copies it out with one
+// contiguous D2H; sg_read_records copies the chunk's wire image in, takes it
+// apart in HBM and copies the plaintext out contiguously.
 std::mutex g_reg_mu;
 std::vector<std::pair<uintptr_t, uintptr_t>> g_reg;  // [lo, hi)
 bool registered(const void* p, size_t n) {
@@ -349,9 +352,7 @@ int64_t sg_write_records(sg_ctx* c, uint64_t seq0, uint8_t content_type, uint8_t
             h[2] = ver_minor;
             put_be16(h + 3, rec_len(r) + SG_MAC_LEN);
         };
-        if (zc) {
-            for (uint32_t i = 0; i < s.nrec; ++i) header(s.first + i);
-        } else {
+        if (!zc) {
             copy_run(s.nrec, [&](uint32_t i) {
                 const uint64_t r = s.first + i;
                 header(r);
@@ -422,16 +423,15 @@ int64_t sg_write_records(sg_ctx* c, uint64_t seq0, uint8_t content_type, uint8_t
             if ((rc = sg_seal_batch(&b)) != SG_OK) return rc;
             SG_HIP(hipEventRecord(s.ev[2], s.st));
             if (zc) {
-                // fragments (ct || tag) into their wire slots: full records with one
-                // strided copy (pitch kWireRec), the partial last record alone
-                const uint32_t full = s.h_len[k - 1] == SG_RECORD_MAX_LEN ? k : k - 1;
-                uint8_t* w0 = wire + next * kWireRec + SG_HEADER_LEN;
-                if (full)
-                    SG_HIP(hipMemcpy2DAsync(w0, kWireRec, s.d_out, kSlot, SG_RECORD_MAX_LEN + SG_MAC_LEN, full,
-                                            hipMemcpyDeviceToHost, s.st));
-                if (full < k)
-                    SG_HIP(hipMemcpyAsync(w0 + (size_t)full * kWireRec, s.d_out + (size_t)full * kSlot,
-                                          s.h_len[k - 1] + SG_MAC_LEN, hipMemcpyDeviceToHost, s.st));
+                // the chunk's wire image (headers and fragments, tls.rs:126-130) is
+                // built in HBM and leaves in one contiguous copy (a strided copy at
+                // the wire's pitch was ~50x slower on the host link)
+                const uint32_t last = s.h_len[k - 1] + SG_MAC_LEN;
+                const uint32_t hdr = content_type | ((uint32_t)ver_major << 8) | ((uint32_t)ver_minor << 16);
+                SG_HIP(launch_frame(s.d_out, kSlot, s.d_wire, (uint32_t)kWireRec, k, SG_RECORD_MAX_LEN + SG_MAC_LEN, last,
+                                    hdr, s.st));
+                SG_HIP(hipMemcpyAsync(wire + next * kWireRec, s.d_wire, (size_t)(k - 1) * kWireRec + SG_HEADER_LEN + last,
+                                      hipMemcpyDeviceToHost, s.st));
             } else {
                 SG_HIP(hipMemcpyAsync(s.h_out, s.d_out, (size_t)k * kSlot, hipMemcpyDeviceToHost, s.st));
             }
@@ -580,9 +580,11 @@ int sg_read_records(sg_ctx* c, uint64_t seq0, const uint8_t* wire, size_t wire_l
             }
             t_host += now_ms() - t0;
             SG_HIP(hipEventRecord(s.ev[0], s.st));
-            if (czc) {  // the fragments, one strided copy out of the wire
-                SG_HIP(hipMemcpy2DAsync(s.d_in, kSlot, wire + R0.off, SG_HEADER_LEN + R0.flen, R0.flen, k,
-                                        hipMemcpyHostToDevice, s.st));
+            if (czc) {  // the chunk's wire image in one contiguous copy, taken apart in HBM
+                const uint32_t pitch = SG_HEADER_LEN + R0.flen;
+                SG_HIP(hipMemcpyAsync(s.d_wire, wire + R0.off - SG_HEADER_LEN, (size_t)k * pitch, hipMemcpyHostToDevice,
+                                      s.st));
+                SG_HIP(launch_unframe(s.d_wire, pitch, s.d_in, kSlot, k, R0.flen, s.st));
             } else {
                 SG_HIP(hipMemcpyAsync(s.d_in, s.h_in, (size_t)k * kSlot, hipMemcpyHostToDevice, s.st));
                 if (!same) SG_HIP(hipMemcpyAsync(s.d_len, s.h_len, k * 4u, hipMemcpyHostToDevice, s.st));
