@@ -155,10 +155,19 @@ struct RecordStaging {
         uint64_t first = 0;      // index of its first record in the call
         bool busy = false;
     } slot[2];
+    // the host-link copies of both slots, one stream per direction, so that
+    // one slot's H2D and the other's D2H run on different DMA engines at once
+    // (with each slot's copies on its own stream they went one after the other)
+    hipStream_t h2d = nullptr, d2h = nullptr;
 };
 
 void record_staging_free(RecordStaging* rs) {
     if (!rs) return;
+    for (hipStream_t cs : {rs->h2d, rs->d2h})
+        if (cs) {
+            (void)hipStreamSynchronize(cs);
+            (void)hipStreamDestroy(cs);
+        }
     for (auto& s : rs->slot) {
         if (s.st) (void)hipStreamSynchronize(s.st);
         (void)hipHostFree(s.h_in);
@@ -203,6 +212,8 @@ int staging(sg_ctx* c, RecordStaging** out) {
             SG_HIP(hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking));
             for (auto& e : s.ev) SG_HIP(hipEventCreate(&e));
         }
+        SG_HIP(hipStreamCreateWithFlags(&rs->h2d, hipStreamNonBlocking));
+        SG_HIP(hipStreamCreateWithFlags(&rs->d2h, hipStreamNonBlocking));
     }
     *out = c->rec;
     return SG_OK;
@@ -230,6 +241,11 @@ struct SlotReset {
     explicit SlotReset(RecordStaging* r) : rs(r) { reset(); }
     ~SlotReset() { reset(); }
     void reset() {
+        const bool any = rs->slot[0].busy || rs->slot[1].busy;
+        if (any) {
+            if (rs->h2d) (void)hipStreamSynchronize(rs->h2d);
+            if (rs->d2h) (void)hipStreamSynchronize(rs->d2h);
+        }
         for (auto& s : rs->slot) {
             if (s.busy && s.st) (void)hipStreamSynchronize(s.st);
             s.busy = false;
@@ -390,15 +406,17 @@ int64_t sg_write_records(sg_ctx* c, uint64_t seq0, uint8_t content_type, uint8_t
             for (uint32_t i = 1; i < k; ++i) same = same && s.h_len[i] == s.h_len[0];
             t_host += now_ms() - t0;
             const size_t in_stride = zc ? SG_RECORD_MAX_LEN : kSlot;
-            SG_HIP(hipEventRecord(s.ev[0], s.st));
+            hipStream_t hs = rs->h2d, ds = rs->d2h;
+            SG_HIP(hipEventRecord(s.ev[0], hs));
             if (zc) {
                 const size_t bytes = (size_t)(k - 1) * SG_RECORD_MAX_LEN + s.h_len[k - 1];
-                SG_HIP(hipMemcpyAsync(s.d_in, data + next * SG_RECORD_MAX_LEN, bytes, hipMemcpyHostToDevice, s.st));
+                SG_HIP(hipMemcpyAsync(s.d_in, data + next * SG_RECORD_MAX_LEN, bytes, hipMemcpyHostToDevice, hs));
             } else {
-                SG_HIP(hipMemcpyAsync(s.d_in, s.h_in, (size_t)k * kSlot, hipMemcpyHostToDevice, s.st));
+                SG_HIP(hipMemcpyAsync(s.d_in, s.h_in, (size_t)k * kSlot, hipMemcpyHostToDevice, hs));
             }
-            if (!same) SG_HIP(hipMemcpyAsync(s.d_len, s.h_len, k * 4u, hipMemcpyHostToDevice, s.st));
-            SG_HIP(hipEventRecord(s.ev[1], s.st));
+            if (!same) SG_HIP(hipMemcpyAsync(s.d_len, s.h_len, k * 4u, hipMemcpyHostToDevice, hs));
+            SG_HIP(hipEventRecord(s.ev[1], hs));
+            SG_HIP(hipStreamWaitEvent(s.st, s.ev[1], 0));
             sg_batch b;
             std::memset(&b, 0, sizeof b);
             b.count = k;
@@ -421,21 +439,24 @@ int64_t sg_write_records(sg_ctx* c, uint64_t seq0, uint8_t content_type, uint8_t
             b.workspace = s.d_ws;
             b.workspace_size = sg_workspace_size(kChunk);
             if ((rc = sg_seal_batch(&b)) != SG_OK) return rc;
-            SG_HIP(hipEventRecord(s.ev[2], s.st));
+            const uint32_t last = s.h_len[k - 1] + SG_MAC_LEN;
             if (zc) {
                 // the chunk's wire image (headers and fragments, tls.rs:126-130) is
                 // built in HBM and leaves in one contiguous copy (a strided copy at
                 // the wire's pitch was ~50x slower on the host link)
-                const uint32_t last = s.h_len[k - 1] + SG_MAC_LEN;
                 const uint32_t hdr = content_type | ((uint32_t)ver_major << 8) | ((uint32_t)ver_minor << 16);
                 SG_HIP(launch_frame(s.d_out, kSlot, s.d_wire, (uint32_t)kWireRec, k, SG_RECORD_MAX_LEN + SG_MAC_LEN, last,
                                     hdr, s.st));
-                SG_HIP(hipMemcpyAsync(wire + next * kWireRec, s.d_wire, (size_t)(k - 1) * kWireRec + SG_HEADER_LEN + last,
-                                      hipMemcpyDeviceToHost, s.st));
-            } else {
-                SG_HIP(hipMemcpyAsync(s.h_out, s.d_out, (size_t)k * kSlot, hipMemcpyDeviceToHost, s.st));
             }
-            SG_HIP(hipEventRecord(s.ev[3], s.st));
+            SG_HIP(hipEventRecord(s.ev[2], s.st));
+            SG_HIP(hipStreamWaitEvent(ds, s.ev[2], 0));
+            if (zc) {
+                SG_HIP(hipMemcpyAsync(wire + next * kWireRec, s.d_wire, (size_t)(k - 1) * kWireRec + SG_HEADER_LEN + last,
+                                      hipMemcpyDeviceToHost, ds));
+            } else {
+                SG_HIP(hipMemcpyAsync(s.h_out, s.d_out, (size_t)k * kSlot, hipMemcpyDeviceToHost, ds));
+            }
+            SG_HIP(hipEventRecord(s.ev[3], ds));
             s.nrec = k;
             s.first = next;
             s.busy = true;
@@ -579,22 +600,24 @@ int sg_read_records(sg_ctx* c, uint64_t seq0, const uint8_t* wire, size_t wire_l
                 }
             }
             t_host += now_ms() - t0;
-            SG_HIP(hipEventRecord(s.ev[0], s.st));
+            hipStream_t hs = rs->h2d, ds = rs->d2h;
+            SG_HIP(hipEventRecord(s.ev[0], hs));
+            const uint32_t pitch = SG_HEADER_LEN + R0.flen;
             if (czc) {  // the chunk's wire image in one contiguous copy, taken apart in HBM
-                const uint32_t pitch = SG_HEADER_LEN + R0.flen;
                 SG_HIP(hipMemcpyAsync(s.d_wire, wire + R0.off - SG_HEADER_LEN, (size_t)k * pitch, hipMemcpyHostToDevice,
-                                      s.st));
-                SG_HIP(launch_unframe(s.d_wire, pitch, s.d_in, kSlot, k, R0.flen, s.st));
+                                      hs));
             } else {
-                SG_HIP(hipMemcpyAsync(s.d_in, s.h_in, (size_t)k * kSlot, hipMemcpyHostToDevice, s.st));
-                if (!same) SG_HIP(hipMemcpyAsync(s.d_len, s.h_len, k * 4u, hipMemcpyHostToDevice, s.st));
+                SG_HIP(hipMemcpyAsync(s.d_in, s.h_in, (size_t)k * kSlot, hipMemcpyHostToDevice, hs));
+                if (!same) SG_HIP(hipMemcpyAsync(s.d_len, s.h_len, k * 4u, hipMemcpyHostToDevice, hs));
             }
             if (!tls) {
-                SG_HIP(hipMemcpyAsync(s.d_meta, s.h_meta, 8u * k, hipMemcpyHostToDevice, s.st));
+                SG_HIP(hipMemcpyAsync(s.d_meta, s.h_meta, 8u * k, hipMemcpyHostToDevice, hs));
                 SG_HIP(hipMemcpyAsync(s.d_meta + 8u * kChunk, s.h_meta + 8u * kChunk, 13u * k, hipMemcpyHostToDevice,
-                                      s.st));
+                                      hs));
             }
-            SG_HIP(hipEventRecord(s.ev[1], s.st));
+            SG_HIP(hipEventRecord(s.ev[1], hs));
+            SG_HIP(hipStreamWaitEvent(s.st, s.ev[1], 0));
+            if (czc) SG_HIP(launch_unframe(s.d_wire, pitch, s.d_in, kSlot, k, R0.flen, s.st));
             sg_batch b;
             std::memset(&b, 0, sizeof b);
             b.count = k;
@@ -631,13 +654,14 @@ int sg_read_records(sg_ctx* c, uint64_t seq0, const uint8_t* wire, size_t wire_l
             if (!czc) b.flags |= SG_BATCH_KEEP_FAILED;
             if ((rc = sg_open_batch(&b)) != SG_OK) return rc;
             SG_HIP(hipEventRecord(s.ev[2], s.st));
+            SG_HIP(hipStreamWaitEvent(ds, s.ev[2], 0));
             if (czc) {
-                SG_HIP(hipMemcpyAsync(out + pre[next], s.d_out, pre[next + k] - pre[next], hipMemcpyDeviceToHost, s.st));
+                SG_HIP(hipMemcpyAsync(out + pre[next], s.d_out, pre[next + k] - pre[next], hipMemcpyDeviceToHost, ds));
             } else {
-                SG_HIP(hipMemcpyAsync(s.h_out, s.d_out, (size_t)k * kSlot, hipMemcpyDeviceToHost, s.st));
+                SG_HIP(hipMemcpyAsync(s.h_out, s.d_out, (size_t)k * kSlot, hipMemcpyDeviceToHost, ds));
             }
-            SG_HIP(hipMemcpyAsync(s.h_status, s.d_status, k, hipMemcpyDeviceToHost, s.st));
-            SG_HIP(hipEventRecord(s.ev[3], s.st));
+            SG_HIP(hipMemcpyAsync(s.h_status, s.d_status, k, hipMemcpyDeviceToHost, ds));
+            SG_HIP(hipEventRecord(s.ev[3], ds));
             s.nrec = k;
             s.first = next;
             s.busy = true;
