@@ -155,19 +155,45 @@ struct RecordStaging {
         uint64_t first = 0;      // index of its first record in the call
         bool busy = false;
     } slot[2];
-    // the host-link copies of both slots, one stream per direction, so that
-    // one slot's H2D and the other's D2H run on different DMA engines at once
-    // (with each slot's copies on its own stream they went one after the other)
-    hipStream_t h2d = nullptr, d2h = nullptr;
 };
+
+// Stream layout of the pipeline.  Mode 0 (default): each slot's copies and
+// kernels on the slot's stream.  Mode 1 (SG_COPY_STREAMS=1, experiment): the
+// host-link copies of every context on one process-wide stream per direction
+// and each context's kernels on its slot-0 stream, so that one slot's H2D can
+// run beside the other's D2H on different DMA engines while the process stays
+// within a few hardware queues (GPU_MAX_HW_QUEUES = 4: more streams than that
+// share queues and serialise).
+struct PipeStreams {
+    hipStream_t h2d, krn, d2h;
+};
+int copy_streams_mode() {
+    static const int m = [] {
+        const char* e = std::getenv("SG_COPY_STREAMS");
+        return e && e[0] == '1' ? 1 : 0;
+    }();
+    return m;
+}
+std::mutex g_cs_mu;
+std::vector<std::pair<int, std::pair<hipStream_t, hipStream_t>>> g_copy_streams;  // device -> (h2d, d2h)
+hipError_t process_copy_streams(int dev, hipStream_t* h2d, hipStream_t* d2h) {
+    std::lock_guard<std::mutex> lk(g_cs_mu);
+    for (auto& e : g_copy_streams)
+        if (e.first == dev) {
+            *h2d = e.second.first;
+            *d2h = e.second.second;
+            return hipSuccess;
+        }
+    hipError_t e;
+    if ((e = hipStreamCreateWithFlags(h2d, hipStreamNonBlocking)) != hipSuccess) return e;
+    if ((e = hipStreamCreateWithFlags(d2h, hipStreamNonBlocking)) != hipSuccess) return e;
+    g_copy_streams.push_back({dev, {*h2d, *d2h}});
+    return hipSuccess;
+}
 
 void record_staging_free(RecordStaging* rs) {
     if (!rs) return;
-    for (hipStream_t cs : {rs->h2d, rs->d2h})
-        if (cs) {
-            (void)hipStreamSynchronize(cs);
-            (void)hipStreamDestroy(cs);
-        }
+
     for (auto& s : rs->slot) {
         if (s.st) (void)hipStreamSynchronize(s.st);
         (void)hipHostFree(s.h_in);
@@ -212,8 +238,6 @@ int staging(sg_ctx* c, RecordStaging** out) {
             SG_HIP(hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking));
             for (auto& e : s.ev) SG_HIP(hipEventCreate(&e));
         }
-        SG_HIP(hipStreamCreateWithFlags(&rs->h2d, hipStreamNonBlocking));
-        SG_HIP(hipStreamCreateWithFlags(&rs->d2h, hipStreamNonBlocking));
     }
     *out = c->rec;
     return SG_OK;
@@ -238,22 +262,36 @@ int drain(RecordStaging::Slot& s) {
 // with its own lengths and sequence numbers, to the next call.
 struct SlotReset {
     RecordStaging* rs;
-    explicit SlotReset(RecordStaging* r) : rs(r) { reset(); }
+    PipeStreams ps[2];
+    explicit SlotReset(RecordStaging* r) : rs(r) {
+        for (auto& p : ps) p = {nullptr, nullptr, nullptr};
+        reset();
+    }
     ~SlotReset() { reset(); }
     void reset() {
-        const bool any = rs->slot[0].busy || rs->slot[1].busy;
-        if (any) {
-            if (rs->h2d) (void)hipStreamSynchronize(rs->h2d);
-            if (rs->d2h) (void)hipStreamSynchronize(rs->d2h);
-        }
-        for (auto& s : rs->slot) {
-            if (s.busy && s.st) (void)hipStreamSynchronize(s.st);
+        for (int i = 0; i < 2; ++i) {
+            auto& s = rs->slot[i];
+            if (s.busy)
+                for (hipStream_t t : {ps[i].h2d, ps[i].krn, ps[i].d2h, s.st})
+                    if (t) (void)hipStreamSynchronize(t);
             s.busy = false;
             s.nrec = 0;
             s.first = 0;
         }
     }
 };
+
+// the streams of slot i for this call (mode: copy_streams_mode)
+int pipe_streams(sg_ctx* c, RecordStaging* rs, int i, PipeStreams* out) {
+    if (copy_streams_mode() == 0) {
+        *out = {rs->slot[i].st, rs->slot[i].st, rs->slot[i].st};
+        return SG_OK;
+    }
+    hipStream_t h = nullptr, d = nullptr;
+    SG_HIP(process_copy_streams(c->device, &h, &d));
+    *out = {h, rs->slot[0].st, d};
+    return SG_OK;
+}
 
 inline void put_be16(uint8_t* p, uint32_t v) {
     p[0] = (uint8_t)(v >> 8);
@@ -348,6 +386,8 @@ int64_t sg_write_records(sg_ctx* c, uint64_t seq0, uint8_t content_type, uint8_t
     int rc = staging(c, &rs);
     if (rc != SG_OK) return rc;
     SlotReset slot_reset(rs);
+    for (int i = 0; i < 2; ++i)
+        if ((rc = pipe_streams(c, rs, i, &slot_reset.ps[i])) != SG_OK) return rc;
     size_t wpos = 0;
     // every record but the last is full, so record r starts at r * kWireRec
     constexpr size_t kWireRec = SG_HEADER_LEN + SG_RECORD_MAX_LEN + SG_MAC_LEN;
@@ -406,7 +446,8 @@ int64_t sg_write_records(sg_ctx* c, uint64_t seq0, uint8_t content_type, uint8_t
             for (uint32_t i = 1; i < k; ++i) same = same && s.h_len[i] == s.h_len[0];
             t_host += now_ms() - t0;
             const size_t in_stride = zc ? SG_RECORD_MAX_LEN : kSlot;
-            hipStream_t hs = rs->h2d, ds = rs->d2h;
+            const PipeStreams& P = slot_reset.ps[cur];
+            hipStream_t hs = P.h2d, ks = P.krn, ds = P.d2h;
             SG_HIP(hipEventRecord(s.ev[0], hs));
             if (zc) {
                 const size_t bytes = (size_t)(k - 1) * SG_RECORD_MAX_LEN + s.h_len[k - 1];
@@ -416,7 +457,7 @@ int64_t sg_write_records(sg_ctx* c, uint64_t seq0, uint8_t content_type, uint8_t
             }
             if (!same) SG_HIP(hipMemcpyAsync(s.d_len, s.h_len, k * 4u, hipMemcpyHostToDevice, hs));
             SG_HIP(hipEventRecord(s.ev[1], hs));
-            SG_HIP(hipStreamWaitEvent(s.st, s.ev[1], 0));
+            if (ks != hs) SG_HIP(hipStreamWaitEvent(ks, s.ev[1], 0));
             sg_batch b;
             std::memset(&b, 0, sizeof b);
             b.count = k;
@@ -435,7 +476,7 @@ int64_t sg_write_records(sg_ctx* c, uint64_t seq0, uint8_t content_type, uint8_t
             b.len = same ? nullptr : s.d_len;
             b.uniform_len = same ? s.h_len[0] : 0u;
             b.max_len = SG_RECORD_MAX_LEN;
-            b.stream = s.st;
+            b.stream = ks;
             b.workspace = s.d_ws;
             b.workspace_size = sg_workspace_size(kChunk);
             if ((rc = sg_seal_batch(&b)) != SG_OK) return rc;
@@ -446,10 +487,10 @@ int64_t sg_write_records(sg_ctx* c, uint64_t seq0, uint8_t content_type, uint8_t
                 // the wire's pitch was ~50x slower on the host link)
                 const uint32_t hdr = content_type | ((uint32_t)ver_major << 8) | ((uint32_t)ver_minor << 16);
                 SG_HIP(launch_frame(s.d_out, kSlot, s.d_wire, (uint32_t)kWireRec, k, SG_RECORD_MAX_LEN + SG_MAC_LEN, last,
-                                    hdr, s.st));
+                                    hdr, ks));
             }
-            SG_HIP(hipEventRecord(s.ev[2], s.st));
-            SG_HIP(hipStreamWaitEvent(ds, s.ev[2], 0));
+            SG_HIP(hipEventRecord(s.ev[2], ks));
+            if (ds != ks) SG_HIP(hipStreamWaitEvent(ds, s.ev[2], 0));
             if (zc) {
                 SG_HIP(hipMemcpyAsync(wire + next * kWireRec, s.d_wire, (size_t)(k - 1) * kWireRec + SG_HEADER_LEN + last,
                                       hipMemcpyDeviceToHost, ds));
@@ -495,6 +536,8 @@ int sg_read_records(sg_ctx* c, uint64_t seq0, const uint8_t* wire, size_t wire_l
     int rc = staging(c, &rs);
     if (rc != SG_OK) return rc;
     SlotReset slot_reset(rs);
+    for (int i = 0; i < 2; ++i)
+        if ((rc = pipe_streams(c, rs, i, &slot_reset.ps[i])) != SG_OK) return rc;
 
     const uint64_t nrec = recs.size();
     uint64_t next = 0, good = 0, opos = 0, consumed = 0;
@@ -600,7 +643,8 @@ int sg_read_records(sg_ctx* c, uint64_t seq0, const uint8_t* wire, size_t wire_l
                 }
             }
             t_host += now_ms() - t0;
-            hipStream_t hs = rs->h2d, ds = rs->d2h;
+            const PipeStreams& P = slot_reset.ps[cur];
+            hipStream_t hs = P.h2d, ks = P.krn, ds = P.d2h;
             SG_HIP(hipEventRecord(s.ev[0], hs));
             const uint32_t pitch = SG_HEADER_LEN + R0.flen;
             if (czc) {  // the chunk's wire image in one contiguous copy, taken apart in HBM
@@ -616,8 +660,8 @@ int sg_read_records(sg_ctx* c, uint64_t seq0, const uint8_t* wire, size_t wire_l
                                       hs));
             }
             SG_HIP(hipEventRecord(s.ev[1], hs));
-            SG_HIP(hipStreamWaitEvent(s.st, s.ev[1], 0));
-            if (czc) SG_HIP(launch_unframe(s.d_wire, pitch, s.d_in, kSlot, k, R0.flen, s.st));
+            if (ks != hs) SG_HIP(hipStreamWaitEvent(ks, s.ev[1], 0));
+            if (czc) SG_HIP(launch_unframe(s.d_wire, pitch, s.d_in, kSlot, k, R0.flen, ks));
             sg_batch b;
             std::memset(&b, 0, sizeof b);
             b.count = k;
@@ -644,7 +688,7 @@ int sg_read_records(sg_ctx* c, uint64_t seq0, const uint8_t* wire, size_t wire_l
             b.uniform_len = same ? R0.flen : 0u;
             b.max_len = SG_ENC_RECORD_MAX_LEN;
             b.status = s.d_status;
-            b.stream = s.st;
+            b.stream = ks;
             b.workspace = s.d_ws;
             b.workspace_size = sg_workspace_size(kChunk);
             // staged: the reader delivers nothing from a failed record (it stops
@@ -653,8 +697,8 @@ int sg_read_records(sg_ctx* c, uint64_t seq0, const uint8_t* wire, size_t wire_l
             // scrubbed on the device first
             if (!czc) b.flags |= SG_BATCH_KEEP_FAILED;
             if ((rc = sg_open_batch(&b)) != SG_OK) return rc;
-            SG_HIP(hipEventRecord(s.ev[2], s.st));
-            SG_HIP(hipStreamWaitEvent(ds, s.ev[2], 0));
+            SG_HIP(hipEventRecord(s.ev[2], ks));
+            if (ds != ks) SG_HIP(hipStreamWaitEvent(ds, s.ev[2], 0));
             if (czc) {
                 SG_HIP(hipMemcpyAsync(out + pre[next], s.d_out, pre[next + k] - pre[next], hipMemcpyDeviceToHost, ds));
             } else {
