@@ -157,20 +157,23 @@ struct RecordStaging {
     } slot[2];
 };
 
-// Stream layout of the pipeline.  Mode 0 (default): each slot's copies and
-// kernels on the slot's stream.  Mode 1 (SG_COPY_STREAMS=1, experiment): the
-// host-link copies of every context on one process-wide stream per direction
-// and each context's kernels on its slot-0 stream, so that one slot's H2D can
-// run beside the other's D2H on different DMA engines while the process stays
-// within a few hardware queues (GPU_MAX_HW_QUEUES = 4: more streams than that
-// share queues and serialise).
+// Stream layout of the pipeline.  Mode 1 (default): the host-link copies of
+// every context on one process-wide stream per direction and each context's
+// kernels on its slot-0 stream, so that one slot's H2D runs beside the other's
+// D2H on different DMA engines while the process stays within a few hardware
+// queues (GPU_MAX_HW_QUEUES = 4: more streams than that share queues and
+// serialise; per-context copy streams made two concurrent contexts slower than
+// one after the other).  Same box, 1 GiB per direction, 8 copy threads
+// (profiles/r05g): registered buffers 17.4 -> 27.6 GiB/s write, 23.4 -> 25.8
+// read; pageable 12.6 -> 15.2 write, 15.8 -> 14.5 read.  Mode 0
+// (SG_COPY_STREAMS=0): each slot's copies and kernels on the slot's stream.
 struct PipeStreams {
     hipStream_t h2d, krn, d2h;
 };
 int copy_streams_mode() {
     static const int m = [] {
         const char* e = std::getenv("SG_COPY_STREAMS");
-        return e && e[0] == '1' ? 1 : 0;
+        return e && e[0] == '0' ? 0 : 1;
     }();
     return m;
 }
