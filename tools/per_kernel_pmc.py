@@ -29,7 +29,7 @@ def main(tag: str, out: str | None = None):
             acc[k][c].append(v)
     res = {}
     for k, cs in acc.items():
-        short = k.split("(")[0].replace("void sg::(anonymous namespace)::", "").replace("sg::(anonymous namespace)::", "")
+        short = k.replace("void sg::(anonymous namespace)::", "").replace("sg::(anonymous namespace)::", "").split("(")[0]
         res[short] = {c: round(sum(v) / len(v), 1) for c, v in cs.items()}
         res[short]["dispatches"] = max(len(v) for v in cs.values())
     print(json.dumps(res, indent=1))
