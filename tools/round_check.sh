@@ -18,10 +18,30 @@ import json, sys
 for w in ("c1", "c2"):
     j = json.loads(open(f"{sys.argv[1]}/bench_{w}.json").read().strip().splitlines()[-1])
     print(w, j["value"], "ms/step", j["ms_per_step"], "frac", j["roofline"]["frac"], "kernel_ms", j["kernel_ms"]["seal"],
-          j["kernel_ms"]["open"], j["kernel_ms"]["keying"], "correct", j["correct"], "cpu", (j["cpu_baseline"] or {}).get("value"))
+          j["kernel_ms"]["open"], j["kernel_ms"]["keying"], "correct", j["correct"], "cpu", (j["cpu_baseline"] or {}).get("value"),
+          "traffic", j["roofline"].get("traffic"), "valu", (j.get("valu_roofline") or {}).get("frac"),
+          "uJ", j.get("energy_per_record_uj"))
+    if "c2" in j:
+        c = j["c2"]
+        print("  c2 sub-record", c["value"], "frac", c["roofline"]["frac"], "traffic", c["roofline"].get("traffic"),
+              "valu", (c.get("valu_roofline") or {}).get("frac"), "correct", c["correct"], "fold", c.get("bitexact_fold"))
 PY
 # C4 host side and the loopback stream with the same build (round 4)
-timeout -k 10 600 python -u tools/record_path_bench.py --json-out "$OUT/record_path.json" > "$OUT/record_path.log" 2>&1 || echo "record_path failed"
+timeout -k 10 600 python -u tools/record_path_bench.py --registered 0,1 --json-out "$OUT/record_path.json" > "$OUT/record_path.log" 2>&1 || echo "record_path failed"
 tail -c 400 "$OUT/record_path.log"; echo
 timeout -k 10 600 python -u tools/tls_loopback.py --json-out "$OUT/loopback.json" --watchdog 500 > "$OUT/loopback.log" 2>&1 || echo "loopback failed"
 tail -c 400 "$OUT/loopback.log"; echo
+# C4 from C++ (round 5): staged and registered (zero-copy) buffers
+for m in "" "--registered"; do
+  tag=loopback_cpp${m:+_reg}
+  timeout -k 10 300 ./tools/loopback_cpp $m --json-out "$OUT/$tag.json" > /dev/null 2> "$OUT/$tag.err" || echo "$tag failed"
+done
+python -c "
+import json
+for f in ('loopback_cpp', 'loopback_cpp_reg'):
+    try:
+        j = json.load(open('$OUT/' + f + '.json')); print(f, j['gibs'], j['correct'])
+    except OSError as e:
+        print(f, 'missing', e)
+"
+
