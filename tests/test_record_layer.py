@@ -355,3 +355,73 @@ def test_gpu_zero_copy_record_path(gpu, oracle):
     finally:
         for a in (data, wire, out):
             N.check(lib.sg_host_unregister(a.ctypes.data))
+
+
+@pytest.mark.gpu
+def test_gpu_zero_copy_edges(gpu, oracle):
+    """Registered-buffer edges: a write shorter than one record, and a read
+    whose second chunk mixes content types (equal, back-to-back fragments: the
+    wire image is still copied in whole and taken apart in HBM, but nonce and
+    AD go explicit, tls.rs:250-265).  Both equal the staged path byte for
+    byte; the types come back per record."""
+    import ctypes as C
+
+    import numpy as np
+
+    from suruga_amd import ChaCha20Poly1305
+    from suruga_amd import _native as N
+
+    lib = N.load()
+    key = bytes(range(3, 35))
+    enc, dec = ChaCha20Poly1305().new_encryptor(key), ChaCha20Poly1305().new_decryptor(key)
+
+    # (a) 100 bytes: one short record, zero-copy against staged
+    small = np.frombuffer(oracle.fill_record(0x11, 1, 100), dtype=np.uint8).copy()
+    cap = lib.sg_wire_bound(100)
+    staged, wire = np.zeros(cap, dtype=np.uint8), np.zeros(cap, dtype=np.uint8)
+    wl = C.c_size_t(0)
+    assert N.check(lib.sg_write_records(enc._ptr, 9, 23, 3, 3, small.ctypes.data, 100, staged.ctypes.data, cap,
+                                        C.byref(wl))) == 1
+    for a in (small, wire):
+        N.check(lib.sg_host_register(a.ctypes.data, a.nbytes))
+    try:
+        wl2 = C.c_size_t(0)
+        assert N.check(lib.sg_write_records(enc._ptr, 9, 23, 3, 3, small.ctypes.data, 100, wire.ctypes.data, cap,
+                                            C.byref(wl2))) == 1
+        assert wl2.value == wl.value == 5 + 100 + 16 and np.array_equal(wire, staged)
+        assert wire[5:121].tobytes() == oracle.seal(key, struct.pack(">Q", 9), small.tobytes(), oracle.tls_ad(9, 100))
+    finally:
+        for a in (small, wire):
+            N.check(lib.sg_host_unregister(a.ctypes.data))
+
+    # (b) 300 application-data records then 10 handshake records, one stream
+    n1, n2 = 300, 10
+    d1 = np.frombuffer(oracle.fill_record(0x21, 2, n1 * RECORD_MAX_LEN), dtype=np.uint8).copy()
+    d2 = np.frombuffer(oracle.fill_record(0x22, 3, n2 * RECORD_MAX_LEN), dtype=np.uint8).copy()
+    c1, c2 = lib.sg_wire_bound(d1.size), lib.sg_wire_bound(d2.size)
+    w1, w2 = np.zeros(c1, dtype=np.uint8), np.zeros(c2, dtype=np.uint8)
+    l1, l2 = C.c_size_t(0), C.c_size_t(0)
+    N.check(lib.sg_write_records(enc._ptr, 0, 23, 3, 3, d1.ctypes.data, d1.size, w1.ctypes.data, c1, C.byref(l1)))
+    N.check(lib.sg_write_records(enc._ptr, n1, 22, 3, 3, d2.ctypes.data, d2.size, w2.ctypes.data, c2, C.byref(l2)))
+    stream = np.concatenate([w1[:l1.value], w2[:l2.value]])
+    expect = np.concatenate([d1, d2])
+    results = {}
+    for registered in (False, True):
+        out = np.full(expect.size, 0xEE, dtype=np.uint8)
+        types = np.zeros(n1 + n2, dtype=np.uint8)
+        if registered:
+            for a in (stream, out):
+                N.check(lib.sg_host_register(a.ctypes.data, a.nbytes))
+        try:
+            res = N.SgReadResult()
+            N.check(lib.sg_read_records(dec._ptr, 0, stream.ctypes.data, stream.size, out.ctypes.data, out.size,
+                                        types.ctypes.data, None, 1 << 20, C.byref(res)))
+        finally:
+            if registered:
+                for a in (stream, out):
+                    N.check(lib.sg_host_unregister(a.ctypes.data))
+        assert (res.records, res.consumed, res.out_len, res.error) == (n1 + n2, stream.size, expect.size, N.SG_OK)
+        assert np.array_equal(out, expect), registered
+        assert (types[:n1] == 23).all() and (types[n1:] == 22).all()
+        results[registered] = out
+    assert np.array_equal(results[False], results[True])
