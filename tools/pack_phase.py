@@ -42,10 +42,11 @@ def main():
     for _ in range(3):
         B.seal(b)
     torch.cuda.synchronize()
-    buf = (C.c_ulonglong * (8192 * 12))()
+    buf = (C.c_ulonglong * (8192 * 16))()
     n = lib.sg_pack_profile_read(buf, len(buf))
     assert n > 0, n
-    a = np.frombuffer(buf, dtype=np.uint64).reshape(8192, 12).astype(np.int64)
+    cols = n // 8192  # 12 stamps, 16 with the round sums of tools/variants/pk_prof2.py
+    a = np.frombuffer(buf, dtype=np.uint64)[:n].reshape(8192, cols).astype(np.int64)
     a = a[a[:, 0] != 0]
     d = lambda i, j: float(np.mean(a[:, j] - a[:, i]))
     print(f"workgroups {len(a)}  (s_memtime ticks)")
@@ -60,6 +61,12 @@ def main():
     print(f"  wait for the last wave               {d(3, 4):9.0f}")
     print(f"  finish                               {d(4, 5):9.0f}")
     print(f"  whole workgroup                      {d(0, 5):9.0f}")
+    if cols >= 16:
+        nr = float(np.mean(a[:, 15]))
+        print(f"  wave 0's rounds with a chunk         {nr:9.2f}")
+        for j, what in ((12, "before the asm (loads, lookup)"), (13, "ChaCha20 asm (with barriers)"),
+                        (14, "after (FF, XOR, stores, MAC)")):
+            print(f"    per round: {what:31s} {float(np.mean(a[:, j])) / nr:9.0f}")
 
 
 if __name__ == "__main__":
