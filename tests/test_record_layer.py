@@ -425,3 +425,22 @@ def test_gpu_zero_copy_edges(gpu, oracle):
         assert (types[:n1] == 23).all() and (types[n1:] == 22).all()
         results[registered] = out
     assert np.array_equal(results[False], results[True])
+
+
+def test_frame_record_index_math():
+    """sg_frame_kernel finds the wire record of destination byte b as
+    r = (b * rdiv) >> 40, rdiv = ceil(2^40 / pitch) (sg_kernels.hip), for
+    images below 2^24 bytes (launch_frame's guard).  Exact for every pitch a
+    wire record can have (5-byte header + 16..2^14+16 byte fragment, and any
+    pitch below 2^16): the error term b (rdiv pitch - 2^40) / 2^40 stays below
+    1 / pitch; and brute force over every b for the record layer's pitch."""
+    import numpy as np
+
+    limit = 1 << 24
+    for pitch in range(21, 1 << 16):
+        rdiv = -(-(1 << 40) // pitch)
+        assert (limit - 1) * (rdiv * pitch - (1 << 40)) < (1 << 40), pitch
+    pitch = 5 + RECORD_MAX_LEN + 16
+    rdiv = np.uint64(-(-(1 << 40) // pitch))
+    b = np.arange(limit, dtype=np.uint64)
+    assert np.array_equal((b * rdiv) >> np.uint64(40), b // np.uint64(pitch))
