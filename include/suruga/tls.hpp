@@ -344,9 +344,9 @@ private:
 class HostBuffer {
 public:
     HostBuffer(size_t n, bool register_it) : n_(n) {
-        p_ = static_cast<uint8_t*>(std::aligned_alloc(4096, (n + 4095) / 4096 * 4096));
+        p_ = static_cast<uint8_t*>(std::aligned_alloc(4096, (n + 4095) / 4096 * 4096 + (n ? 0 : 4096)));
         if (!p_) throw std::bad_alloc();
-        if (register_it) {
+        if (register_it && n_) {  // (an empty buffer stays unregistered: nothing to move)
             const int rc = sg_host_register(p_, n_);
             if (rc != SG_OK) {
                 std::free(p_);

@@ -99,6 +99,11 @@ static const char* kSurveyVector = "59f90370eca7e79052201d20ee020f66fbc2d9037460
 
 // ---- CPU: the reference's own record tests ---------------------------------
 static void cpu_tests() {
+    {  // HostBuffer (tls.hpp): page-aligned; an empty one is valid and stays unregistered
+        HostBuffer a(100, false), e(0, true);
+        CHECK(a.data() && (reinterpret_cast<uintptr_t>(a.data()) & 4095u) == 0 && a.size() == 100 && !a.registered());
+        CHECK(e.data() && e.size() == 0 && !e.registered());
+    }
     {  // test.rs:41-63 test_change_cipher_spec_message
         VecWriter out;
         TlsWriter w(out);
