@@ -357,7 +357,7 @@ __device__ __forceinline__ void pack_run(const KParams& p, const uint32_t* __res
         if (valid) {
             const uint8_t* src = p.in + io + 64u * j;
             // (plain policy: the nontemporal one measured -1.3 % on C2 for this
-            // kernel's 64-byte lane stride, round 3; SG_PACK_NT_LD / _ST to compare)
+            // kernel's 64-byte lane stride, round 3)
             d0 = pld16(src); d1 = pld16(src + 16); d2 = pld16(src + 32); d3 = pld16(src + 48);
         }
         uint32_t kw[8];

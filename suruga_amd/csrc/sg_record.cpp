@@ -2,12 +2,13 @@
 // sg_read_records): the throughput form of suruga's TlsWriter::write_data and
 // TlsReader::read_record (src/tls.rs:99-147, 217-281).
 //
-// Records move through a per-context pipeline of two slots.  Each slot owns
-// pinned host buffers, device buffers, a stream and a keying workspace; while
-// the GPU seals/opens chunk c on one slot, the CPU frames chunk c-1's output
-// and stages chunk c+1 on the other.  Device layout is always 16-byte aligned
-// (record slot stride kSlot), so the kernels take their vector path; the
-// 5-byte TLS headers are added/stripped by the CPU while copying.
+// Records move through a per-context pipeline of three slots.  Each slot owns
+// device buffers, a keying workspace and (staged path, allocated on first use)
+// pinned host buffers; while the GPU seals/opens chunk c on one slot, chunk
+// c-1's output leaves and chunk c+1 comes in on the others.  Device layout is
+// always 16-byte aligned (record slot stride kSlot), so the kernels take their
+// vector path; the 5-byte TLS headers are added/stripped by the CPU while
+// copying (staged path) or by the frame kernels in HBM (zero-copy path).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -32,6 +33,7 @@ namespace {
 constexpr uint32_t kChunk = 256;                                  // records per pipeline chunk
 constexpr uint32_t kSlot = ((SG_ENC_RECORD_MAX_LEN + 63u) / 64u) * 64u;  // device bytes per record
 constexpr uint32_t kMetaBytes = 8u + 13u;                         // nonce + AD per record (reader)
+constexpr int kMaxSlots = 3;                                      // pipeline depth (record_slots)
 
 thread_local double t_h2d = 0, t_kernel = 0, t_d2h = 0, t_host = 0;
 
@@ -154,13 +156,27 @@ struct RecordStaging {
         uint32_t nrec = 0;       // records in flight on this slot
         uint64_t first = 0;      // index of its first record in the call
         bool busy = false;
-    } slot[2];
+    } slot[kMaxSlots];
 };
+
+// Pipeline depth.  Three slots (default) keep one chunk's H2D, another's
+// kernels and a third's D2H in flight at once, on the three streams of
+// copy_streams_mode 1: with two, a chunk's D2H waited for its own kernels
+// while the next chunk's H2D was already done.  SG_RECORD_SLOTS=2 gives the
+// round-4 two-slot pipeline (A/B).
+int record_slots() {
+    static const int n = [] {
+        const char* e = std::getenv("SG_RECORD_SLOTS");
+        const int v = e ? std::atoi(e) : kMaxSlots;
+        return v < 2 ? 2 : (v > kMaxSlots ? kMaxSlots : v);
+    }();
+    return n;
+}
 
 // Stream layout of the pipeline.  Mode 1 (default): the host-link copies of
 // every context on one process-wide stream per direction and each context's
-// kernels on its slot-0 stream, so that one slot's H2D runs beside the other's
-// D2H on different DMA engines while the process stays within a few hardware
+// kernels on its slot-0 stream, so that one slot's H2D runs beside another's
+// kernels and a third's D2H, the copies on different DMA engines while the process stays within a few hardware
 // queues (GPU_MAX_HW_QUEUES = 4: more streams than that share queues and
 // serialise; per-context copy streams made two concurrent contexts slower than
 // one after the other).  Same box, 1 GiB per direction, 8 copy threads
@@ -225,9 +241,8 @@ int staging(sg_ctx* c, RecordStaging** out) {
         auto* rs = new RecordStaging();
         c->rec = rs;  // freed with the context even if allocation below fails
         const size_t bytes = (size_t)kChunk * kSlot;
-        for (auto& s : rs->slot) {
-            SG_HIP(hipHostMalloc((void**)&s.h_in, bytes, hipHostMallocDefault));
-            SG_HIP(hipHostMalloc((void**)&s.h_out, bytes, hipHostMallocDefault));
+        for (int i = 0; i < record_slots(); ++i) {  // (h_in / h_out: host_staging, on first use)
+            auto& s = rs->slot[i];
             SG_HIP(hipHostMalloc((void**)&s.h_meta, (size_t)kChunk * kMetaBytes, hipHostMallocDefault));
             SG_HIP(hipHostMalloc((void**)&s.h_status, kChunk, hipHostMallocDefault));
             SG_HIP(hipHostMalloc((void**)&s.h_len, kChunk * 4u, hipHostMallocDefault));
@@ -243,6 +258,15 @@ int staging(sg_ctx* c, RecordStaging** out) {
         }
     }
     *out = c->rec;
+    return SG_OK;
+}
+
+// The staged path's pinned blocks of a slot (the zero-copy path never needs
+// them, so a context that only moves registered buffers pins no staging).
+int host_staging(RecordStaging::Slot& s) {
+    const size_t bytes = (size_t)kChunk * kSlot;
+    if (!s.h_in) SG_HIP(hipHostMalloc((void**)&s.h_in, bytes, hipHostMallocDefault));
+    if (!s.h_out) SG_HIP(hipHostMalloc((void**)&s.h_out, bytes, hipHostMallocDefault));
     return SG_OK;
 }
 
@@ -265,14 +289,14 @@ int drain(RecordStaging::Slot& s) {
 // with its own lengths and sequence numbers, to the next call.
 struct SlotReset {
     RecordStaging* rs;
-    PipeStreams ps[2];
+    PipeStreams ps[kMaxSlots];
     explicit SlotReset(RecordStaging* r) : rs(r) {
         for (auto& p : ps) p = {nullptr, nullptr, nullptr};
         reset();
     }
     ~SlotReset() { reset(); }
     void reset() {
-        for (int i = 0; i < 2; ++i) {
+        for (int i = 0; i < kMaxSlots; ++i) {
             auto& s = rs->slot[i];
             if (s.busy)
                 for (hipStream_t t : {ps[i].h2d, ps[i].krn, ps[i].d2h, s.st})
@@ -389,8 +413,14 @@ int64_t sg_write_records(sg_ctx* c, uint64_t seq0, uint8_t content_type, uint8_t
     int rc = staging(c, &rs);
     if (rc != SG_OK) return rc;
     SlotReset slot_reset(rs);
-    for (int i = 0; i < 2; ++i)
+    const int ns = record_slots();
+    for (int i = 0; i < ns; ++i)
         if ((rc = pipe_streams(c, rs, i, &slot_reset.ps[i])) != SG_OK) return rc;
+    auto any_busy = [&] {
+        for (int i = 0; i < ns; ++i)
+            if (rs->slot[i].busy) return true;
+        return false;
+    };
     size_t wpos = 0;
     // every record but the last is full, so record r starts at r * kWireRec
     constexpr size_t kWireRec = SG_HEADER_LEN + SG_RECORD_MAX_LEN + SG_MAC_LEN;
@@ -425,7 +455,7 @@ int64_t sg_write_records(sg_ctx* c, uint64_t seq0, uint8_t content_type, uint8_t
 
     uint64_t next = 0;
     int cur = 0;
-    while (next < nrec || rs->slot[0].busy || rs->slot[1].busy) {
+    while (next < nrec || any_busy()) {
         RecordStaging::Slot& s = rs->slot[cur];
         if (s.busy) {  // oldest chunk first: keeps the wire in record order
             if ((rc = drain(s)) != SG_OK) return rc;
@@ -439,6 +469,7 @@ int64_t sg_write_records(sg_ctx* c, uint64_t seq0, uint8_t content_type, uint8_t
             if (zc) {
                 for (uint32_t i = 0; i < k; ++i) s.h_len[i] = rec_len(next + i);
             } else {
+                if ((rc = host_staging(s)) != SG_OK) return rc;
                 copy_run(k, [&](uint32_t i) {
                     const uint64_t r = next + i;
                     std::memcpy(s.h_in + (size_t)i * kSlot, data + r * SG_RECORD_MAX_LEN, rec_len(r));
@@ -506,7 +537,7 @@ int64_t sg_write_records(sg_ctx* c, uint64_t seq0, uint8_t content_type, uint8_t
             s.busy = true;
             next += k;
         }
-        cur ^= 1;
+        cur = (cur + 1) % ns;
     }
     *wire_len = wpos;
     return (int64_t)nrec;
@@ -539,8 +570,14 @@ int sg_read_records(sg_ctx* c, uint64_t seq0, const uint8_t* wire, size_t wire_l
     int rc = staging(c, &rs);
     if (rc != SG_OK) return rc;
     SlotReset slot_reset(rs);
-    for (int i = 0; i < 2; ++i)
+    const int ns = record_slots();
+    for (int i = 0; i < ns; ++i)
         if ((rc = pipe_streams(c, rs, i, &slot_reset.ps[i])) != SG_OK) return rc;
+    auto any_busy = [&] {
+        for (int i = 0; i < ns; ++i)
+            if (rs->slot[i].busy) return true;
+        return false;
+    };
 
     const uint64_t nrec = recs.size();
     uint64_t next = 0, good = 0, opos = 0, consumed = 0;
@@ -556,7 +593,7 @@ int sg_read_records(sg_ctx* c, uint64_t seq0, const uint8_t* wire, size_t wire_l
         for (uint64_t i = 0; i < nrec; ++i) pre[i + 1] = pre[i] + recs[i].flen - SG_MAC_LEN;
     }
     std::vector<uint64_t> dst_off(kChunk);
-    std::vector<uint8_t> chunk_zc(2, 0);  // per slot: the chunk went the zero-copy way
+    std::vector<uint8_t> chunk_zc(kMaxSlots, 0);  // per slot: the chunk went the zero-copy way
     auto collect = [&](RecordStaging::Slot& s, bool szc) {
         const double t0 = now_ms();
         if (error != SG_OK) {  // stopped earlier: nothing of this chunk is delivered
@@ -600,7 +637,7 @@ int sg_read_records(sg_ctx* c, uint64_t seq0, const uint8_t* wire, size_t wire_l
     };
 
     int cur = 0;
-    while (next < nrec || rs->slot[0].busy || rs->slot[1].busy) {
+    while (next < nrec || any_busy()) {
         RecordStaging::Slot& s = rs->slot[cur];
         if (s.busy) {
             if ((rc = drain(s)) != SG_OK) return rc;
@@ -624,6 +661,7 @@ int sg_read_records(sg_ctx* c, uint64_t seq0, const uint8_t* wire, size_t wire_l
             // TLS mode (nonce and AD built on the device, tls.rs:250-265) when the
             // chunk's records share type and version; else explicit nonce / AD
             if (!czc) {
+                if ((rc = host_staging(s)) != SG_OK) return rc;
                 copy_run(k, [&](uint32_t i) {
                     const Rec& R = recs[next + i];
                     std::memcpy(s.h_in + (size_t)i * kSlot, wire + R.off, R.flen);
@@ -714,7 +752,7 @@ int sg_read_records(sg_ctx* c, uint64_t seq0, const uint8_t* wire, size_t wire_l
             s.busy = true;
             next += k;
         }
-        cur ^= 1;
+        cur = (cur + 1) % ns;
     }
     res->records = good;
     res->consumed = consumed;
