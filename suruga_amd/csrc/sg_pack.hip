@@ -191,8 +191,8 @@ __device__ __forceinline__ void lane_mac(H32& h, const uint32_t d[16], uint32_t 
 #ifndef SG_PACK_PROFILE
 #define SG_PACK_PROFILE 0
 #endif
-constexpr uint32_t kProfWgs = 8192, kProfStamps = 12;
 #if SG_PACK_PROFILE
+constexpr uint32_t kProfWgs = 8192, kProfStamps = 12;
 __device__ unsigned long long g_pack_prof[kProfWgs][kProfStamps];
 #define SG_STAMP(w, k)                                                                              \
     do {                                                                                            \

@@ -346,27 +346,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void sg
 // ---------------------------------------------------------------------------
 // The record kernel.
 // ---------------------------------------------------------------------------
-// Four LDS-DMA loads (global_load_lds_dwordx4, 1 KiB each) of one 4 KiB chunk:
-// instruction k writes LDS bytes [l0 + 1024 k, +1024) from each lane's
-// g0 + 1024 k.  hipcc does not count these loads: the kernel waits for them
-// with its own s_waitcnt vmcnt.
-__device__ __forceinline__ void dma_chunk(uint32_t l0, const uint8_t* g0) {
-    const uint8_t* g1 = g0 + 1024;
-    const uint8_t* g2 = g0 + 2048;
-    const uint8_t* g3 = g0 + 3072;
-    uint32_t keep;
-    asm volatile(
-        "s_mov_b32 %0, m0\n\t"
-        "s_mov_b32 m0, %5\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
-        "s_mov_b32 m0, %6\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, off\n\t"
-        "s_mov_b32 m0, %7\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %3, off\n\t"
-        "s_mov_b32 m0, %8\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %4, off\n\t"
-        "s_mov_b32 m0, %0"
-        : "=&s"(keep)
-        : "v"(g0), "v"(g1), "v"(g2), "v"(g3), "s"(l0), "s"(uniform(l0 + 1024u)), "s"(uniform(l0 + 2048u)), "s"(uniform(l0 + 3072u))
-        : "memory");
-}
-
 // a * b + c mod 2^64 (a signed, b a wave-uniform multiplier) in one
 // v_mad_i64_i32; the _1 form: a + c with c uniform.  The compiler does not see
 // these as instructions: the first use of an MFMA result goes through
@@ -421,8 +400,8 @@ __device__ __forceinline__ F26 reduce_words8(const uint32_t w[8]) {
 #ifndef SG_WPR_PROFILE
 #define SG_WPR_PROFILE 0
 #endif
-constexpr uint32_t kProfPhases = 10, kProfWaves = 4096;
 #if SG_WPR_PROFILE
+constexpr uint32_t kProfPhases = 10, kProfWaves = 4096;
 __device__ unsigned long long g_wpr_prof[kProfWaves][kProfPhases];
 #define SG_TICK(v) const uint64_t v = __builtin_amdgcn_s_memtime()
 #define SG_ACC(k, a, b) prof[k] += (b) - (a)
@@ -896,9 +875,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
 
             // keystream block 64 j + lane + 1 of the frame = block 64 j + lane + 1 - vs / 64 of the
             // record (chacha20_poly1305.rs:52), lock-step rounds
-            const uint32_t ctr = 64u * j + lane + 1u - (vs >> 6);
+            const uint32_t bctr = 64u * j + lane + 1u - (vs >> 6);
             uint32_t x[16];
-            x[12] = ctr;
+            x[12] = bctr;
             u32x4 D[4];
             SG_PIN();
             // first double round: every word but the counter enters from SGPRs
@@ -1038,7 +1017,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
             O[0] = D[0] ^ u32x4{x[0] + kSigma0, x[1] + kSigma1, x[2] + kSigma2, x[3] + kSigma3};
             O[1] = D[1] ^ u32x4{x[4] + kw[0], x[5] + kw[1], x[6] + kw[2], x[7] + kw[3]};
             O[2] = D[2] ^ u32x4{x[8] + kw[4], x[9] + kw[5], x[10] + kw[6], x[11] + kw[7]};
-            O[3] = D[3] ^ u32x4{x[12] + ctr, x[13], x[14] + n14, x[15] + n15};
+            O[3] = D[3] ^ u32x4{x[12] + bctr, x[13], x[14] + n14, x[15] + n15};
             // the MAC reads the ciphertext: received (open) or just produced (seal);
             // the lanes of the frame before the record contribute nothing (i8 0)
 #pragma unroll
