@@ -197,8 +197,10 @@ int sg_open_batch(const sg_batch* b);
 
 /* ---- batched record layer over host memory ------------------------------
  * The throughput form of TlsWriter / TlsReader (tls.rs:68-380): many records
- * per call, pinned double-buffered host<->device staging inside the library,
- * wire format exactly as the reference writes and parses it:
+ * per call, pipelined host<->device copies inside the library (three chunks
+ * of 256 records in flight: one coming in, one in the kernels, one going out;
+ * pinned staging for unregistered buffers), wire format exactly as the
+ * reference writes and parses it:
  *   header = content_type || major || minor || be16(fragment length)
  *   (tls.rs:126-130, 218-236) followed by the fragment (ct || tag).        */
 #define SG_RECORD_MAX_LEN      16384u              /* RECORD_MAX_LEN      tls.rs:32 */
@@ -214,11 +216,12 @@ int sg_open_batch(const sg_batch* b);
  * (hipHostRegister) and records the range.  When sg_write_records' `data` and
  * `wire`, or sg_read_records' `wire` and `out`, both lie inside registered
  * ranges, the record bytes move by DMA straight between those buffers and the
- * device -- no framing copy through the library's pinned staging (the
- * 5-byte headers are written / parsed by the host; sg_read_records takes the
- * zero-copy path for chunks of equal, back-to-back records and clears the
- * plaintext of a failed record and of every record after it in `out`, as it
- * delivers none of them).  Unregister only when no call uses the range.
+ * device -- no framing copy through the library's pinned staging
+ * (sg_write_records builds each chunk's wire image, headers included, in HBM;
+ * sg_read_records parses the headers on the host, takes the zero-copy path for
+ * chunks of equal, back-to-back records, whose wire image it takes apart in
+ * HBM, and clears the plaintext of a failed record and of every record after
+ * it in `out`, as it delivers none of them).  Unregister only when no call uses the range.
  * SG_ZERO_COPY=0 in the environment disables the path.  SG_OK or SG_E_ARG /
  * SG_E_HIP. */
 int sg_host_register(void* p, size_t len);
