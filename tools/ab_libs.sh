@@ -4,7 +4,7 @@
 # Variant libraries live in ablib/ (tools/exp/ does not travel to the GPU box).
 # Usage (GPU box): R=2 bash tools/ab_libs.sh base=- v=ablib/lib_v.so ...
 # BENCH_ARGS: extra bench.py arguments (e.g. --workload c2); AB_ALLOW_WRONG=1 times
-# variants whose output is knowingly wrong (tools/variants/, timing only)
+# variants whose output is knowingly wrong (tools/archive/variants/, timing only)
 set -uo pipefail
 R=${R:-2}
 OUT=${GRAFT_REPO_ROOT:-.}/gpurun_out/ab_libs${AB_TAG:-}

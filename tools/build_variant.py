@@ -9,7 +9,7 @@ the marker "<tree hash>+var:<name>:<hash of the edits and defines>", so that
 a variant never carries the product's identity: _native.load() accepts it
 (named by SURUGA_GPU_LIB) only with SURUGA_ALLOW_VARIANT=1, and bench.py
 prints the loaded library's path and marker in its line.  Timing-only variants (skipped work, wrong output)
-live only in ablib/ and in the edit files under tools/variants/.
+live only in ablib/ and in the edit files under tools/archive/variants/.
 
 Usage: python tools/build_variant.py <name> <edits.py> [-DNAME=V ...]
   edits.py defines EDITS = [(file, old, new[, "all"]), ...]

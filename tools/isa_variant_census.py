@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Static census of the C1 seal kernel's record loop for the product and for
-edited copies (tools/variants/*.py edit files): the difference per variant is
+edited copies (tools/archive/variants/*.py edit files): the difference per variant is
 the instruction count of the part it removes, which DESIGN.md §4.2 tables
 next to the measured time that part costs (the same variants timed on the GPU,
 profiles/r04_ab/).  CPU only.

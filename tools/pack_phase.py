@@ -45,7 +45,7 @@ def main():
     buf = (C.c_ulonglong * (8192 * 16))()
     n = lib.sg_pack_profile_read(buf, len(buf))
     assert n > 0, n
-    cols = n // 8192  # 12 stamps, 16 with the round sums of tools/variants/pk_prof2.py
+    cols = n // 8192  # 12 stamps, 16 with the round sums of tools/archive/variants/pk_prof2.py
     a = np.frombuffer(buf, dtype=np.uint64)[:n].reshape(8192, cols).astype(np.int64)
     a = a[a[:, 0] != 0]
     d = lambda i, j: float(np.mean(a[:, j] - a[:, i]))
