@@ -112,8 +112,13 @@ def provenance_error(got: str, want: str, allow_variant: bool):
     whose sources hash to `want`, else the reason.  Experiment variants
     (tools/build_variant.py, _build.build_library(defines=...)) embed
     "<tree hash>+var:<name>:<edit hash>" and run only on explicit request
-    (SURUGA_ALLOW_VARIANT=1, as tools/ab_libs.sh sets)."""
+    (SURUGA_ALLOW_VARIANT=1, as tools/ab_libs.sh sets).  allow_variant ==
+    "foreign" (SURUGA_ALLOW_VARIANT=foreign) also admits a variant built from an
+    earlier tree -- the A/B of a change against the build before it
+    (tools/build_variant.py with no edits) -- and nothing unmarked."""
     if got == want:
+        return None
+    if allow_variant == "foreign" and "+var:" in got:
         return None
     if got.startswith(want + "+var:"):
         if allow_variant:
@@ -216,7 +221,8 @@ def load(path: Path | None = None) -> C.CDLL:
             from ._build import source_hash
 
             got, want = lib.sg_source_hash().decode(), source_hash()
-            err = provenance_error(got, want, os.environ.get("SURUGA_ALLOW_VARIANT") == "1")
+            av = os.environ.get("SURUGA_ALLOW_VARIANT")
+            err = provenance_error(got, want, "foreign" if av == "foreign" else av == "1")
             if err:
                 raise ImportError(f"{p} {err}")
             global _lib_path

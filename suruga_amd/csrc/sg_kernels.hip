@@ -912,7 +912,11 @@ struct PinnedPop {
 // kernels may still be queued, and a concurrent batch on another caller
 // stream must not queue behind them (calls on different streams are
 // independent, suruga_gpu.h).  A busy pooled stream is skipped and a new one
-// created.
+// created, up to kSideCap per device and priority (two concurrent mixed
+// batches' worth): beyond that the batch runs that part on its own stream
+// (the process has four hardware queues, GPU_MAX_HW_QUEUES, and more streams
+// share them and serialise anyway; advisor r5).
+constexpr int kSideCap = 4;
 std::mutex g_side_mu;
 struct SidePooled {
     int dev, prio;
@@ -920,10 +924,12 @@ struct SidePooled {
     hipEvent_t done;
 };
 std::vector<SidePooled> g_side_free;
+std::vector<std::pair<std::pair<int, int>, int>> g_side_made;  // (device, priority) -> streams created
 struct SideStream {
     hipStream_t s = nullptr;
     hipEvent_t done = nullptr;
     int dev = -1, prio = 0;
+    bool borrowed = false;  // s is the caller's stream (the cap was reached): not pooled, no join
     hipError_t acquire(hipStream_t caller) {
         hipError_t e = hipGetDevice(&dev);
         if (e != hipSuccess) return e;
@@ -938,6 +944,19 @@ struct SideStream {
                 g_side_free.erase(g_side_free.begin() + (long)i);
                 return hipSuccess;
             }
+            int* made = nullptr;
+            for (auto& m : g_side_made)
+                if (m.first.first == dev && m.first.second == prio) made = &m.second;
+            if (!made) {
+                g_side_made.push_back({{dev, prio}, 0});
+                made = &g_side_made.back().second;
+            }
+            if (*made >= kSideCap) {
+                s = caller;
+                borrowed = true;
+                return hipSuccess;
+            }
+            ++*made;
         }
         if ((e = hipStreamCreateWithPriority(&s, hipStreamNonBlocking, prio)) != hipSuccess) {
             s = nullptr;
@@ -951,11 +970,12 @@ struct SideStream {
     }
     // the batch's stream s waits for everything enqueued here so far
     hipError_t join_into(hipStream_t t) const {
+        if (borrowed) return hipSuccess;
         hipError_t e = hipEventRecord(done, s);
         return e != hipSuccess ? e : hipStreamWaitEvent(t, done, 0);
     }
     ~SideStream() {
-        if (!s) return;
+        if (!s || borrowed) return;
         std::lock_guard<std::mutex> lk(g_side_mu);
         g_side_free.push_back({dev, prio, s, done});
     }

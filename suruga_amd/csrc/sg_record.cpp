@@ -151,19 +151,19 @@ struct RecordStaging {
         uint8_t* d_wire = nullptr;  // the chunk's wire image (zero-copy path)
         uint32_t* d_len = nullptr;
         void* d_ws = nullptr;
-        hipStream_t st = nullptr;
+        hipStream_t st = nullptr;  // SG_COPY_STREAMS=0 only: the slot's copies and kernels
         hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};  // start, after H2D, after kernels, after D2H
         uint32_t nrec = 0;       // records in flight on this slot
         uint64_t first = 0;      // index of its first record in the call
+        bool zc = false;         // the chunk goes the zero-copy way
         bool busy = false;
     } slot[kMaxSlots];
 };
 
 // Pipeline depth.  Three slots (default) keep one chunk's H2D, another's
-// kernels and a third's D2H in flight at once, on the three streams of
-// copy_streams_mode 1: with two, a chunk's D2H waited for its own kernels
-// while the next chunk's H2D was already done.  SG_RECORD_SLOTS=2 gives the
-// round-4 two-slot pipeline (A/B).
+// kernels and a third's D2H in flight at once: with two, a chunk's D2H waited
+// for its own kernels while the next chunk's H2D was already done.
+// SG_RECORD_SLOTS=2 gives the round-4 two-slot pipeline (A/B).
 int record_slots() {
     static const int n = [] {
         const char* e = std::getenv("SG_RECORD_SLOTS");
@@ -173,16 +173,21 @@ int record_slots() {
     return n;
 }
 
-// Stream layout of the pipeline.  Mode 1 (default): the host-link copies of
-// every context on one process-wide stream per direction and each context's
-// kernels on its slot-0 stream, so that one slot's H2D runs beside another's
-// kernels and a third's D2H, the copies on different DMA engines while the process stays within a few hardware
-// queues (GPU_MAX_HW_QUEUES = 4: more streams than that share queues and
-// serialise; per-context copy streams made two concurrent contexts slower than
-// one after the other).  Same box, 1 GiB per direction, 8 copy threads
+// Stream layout.  Mode 1 (default): the host-link copies of every context on
+// one process-wide stream per direction and each context's kernels on its
+// slot-0 stream, so that one slot's H2D runs beside another's kernels and a
+// third's D2H, the copies on different DMA engines while the process stays
+// within a few hardware queues (GPU_MAX_HW_QUEUES = 4: more streams than that
+// share queues and serialise).  Same box, 1 GiB per direction, 8 copy threads
 // (profiles/r05g): registered buffers 17.4 -> 27.6 GiB/s write, 23.4 -> 25.8
-// read; pageable 12.6 -> 15.2 write, 15.8 -> 14.5 read.  Mode 0
-// (SG_COPY_STREAMS=0): each slot's copies and kernels on the slot's stream.
+// read; pageable 12.6 -> 15.2 write, 15.8 -> 14.5 read.  Round 6 measured the
+// alternatives for a reader and a writer at once (profiles/r06d): the D2H on a
+// stream of each context's own (the context's spare slot stream) 14.8 instead
+// of 29.7 GiB/s registered read, both copy directions per context 24.2 instead
+// of 31.7 write -- the extra streams share hardware queues -- while with the
+// shared copy streams the two directions at once run 1.06-1.34x faster than one
+// after the other.  Mode 0 (SG_COPY_STREAMS=0): each slot's copies and kernels
+// on the slot's stream.
 struct PipeStreams {
     hipStream_t h2d, krn, d2h;
 };
@@ -270,9 +275,8 @@ int host_staging(RecordStaging::Slot& s) {
     return SG_OK;
 }
 
-// Wait for a slot's work and account its device times.
-int drain(RecordStaging::Slot& s) {
-    SG_HIP(hipEventSynchronize(s.ev[3]));
+// Account a finished slot's device times (H2D, kernels, D2H).
+int account(RecordStaging::Slot& s) {
     float a = 0, b = 0, d = 0;
     SG_HIP(hipEventElapsedTime(&a, s.ev[0], s.ev[1]));
     SG_HIP(hipEventElapsedTime(&b, s.ev[1], s.ev[2]));
@@ -280,12 +284,11 @@ int drain(RecordStaging::Slot& s) {
     t_h2d += a;
     t_kernel += b;
     t_d2h += d;
-    s.busy = false;
     return SG_OK;
 }
 
-// Leaves both pipeline slots idle on every exit path: a call that returns
-// early (a drain or launch error) must not hand a half-finished slot, framed
+// Leaves every pipeline slot idle on every exit path: a call that returns
+// early (a launch or copy error) must not hand a half-finished slot, framed
 // with its own lengths and sequence numbers, to the next call.
 struct SlotReset {
     RecordStaging* rs;
@@ -299,11 +302,12 @@ struct SlotReset {
         for (int i = 0; i < kMaxSlots; ++i) {
             auto& s = rs->slot[i];
             if (s.busy)
-                for (hipStream_t t : {ps[i].h2d, ps[i].krn, ps[i].d2h, s.st})
+                for (hipStream_t t : {ps[i].h2d, ps[i].krn, ps[i].d2h})
                     if (t) (void)hipStreamSynchronize(t);
             s.busy = false;
             s.nrec = 0;
             s.first = 0;
+            s.zc = false;
         }
     }
 };
@@ -318,6 +322,49 @@ int pipe_streams(sg_ctx* c, RecordStaging* rs, int i, PipeStreams* out) {
     SG_HIP(process_copy_streams(c->device, &h, &d));
     *out = {h, rs->slot[0].st, d};
     return SG_OK;
+}
+
+// The pipeline of sg_write_records / sg_read_records.  Chunk k uses slot
+// k % ns and passes four steps: stage (host framing copy on the staged path,
+// the H2D), launch (the kernels, on the device after the H2D), copy_out (the
+// D2H, on the device after the kernels) and finish (host framing, oldest chunk
+// first, once the D2H has completed).  The first three are enqueued together,
+// up to ns chunks ahead of the oldest unfinished one, with the cross-stream
+// order kept on the device (hipStreamWaitEvent), so the host only ever waits
+// for the oldest chunk's D2H.  (Round 6 measured a host-driven form, each step
+// enqueued only once the previous one had completed on the device, so that no
+// stream ever holds a device-side wait: 20.6 / 19.6 GiB/s registered write /
+// read against 33.4 / 30.7 for this form on the same box, profiles/r06c --
+// the host's event polling and late enqueues idled the copy engines.)
+// more(): whether another chunk is to be staged (the reader stops at a failed
+// record).
+template <class Streams, class More, class Stage, class Launch, class CopyOut, class Finish>
+int run_pipeline(RecordStaging* rs, int ns, Streams streams, More more, Stage stage, Launch launch, CopyOut copy_out,
+                 Finish finish) {
+    uint64_t staged = 0, done = 0;
+    auto slot = [&](uint64_t k) -> RecordStaging::Slot& { return rs->slot[k % (uint64_t)ns]; };
+    int rc;
+    for (;;) {
+        if (staged < done + (uint64_t)ns && more()) {
+            RecordStaging::Slot& s = slot(staged);
+            const PipeStreams& P = streams(s);
+            s.busy = true;  // (before the enqueues: SlotReset then drains its streams on an error)
+            if ((rc = stage(s)) != SG_OK) return rc;
+            if (P.krn != P.h2d) SG_HIP(hipStreamWaitEvent(P.krn, s.ev[1], 0));
+            if ((rc = launch(s)) != SG_OK) return rc;
+            if (P.d2h != P.krn) SG_HIP(hipStreamWaitEvent(P.d2h, s.ev[2], 0));
+            if ((rc = copy_out(s)) != SG_OK) return rc;
+            ++staged;
+            continue;
+        }
+        if (done == staged) return SG_OK;
+        RecordStaging::Slot& s = slot(done);
+        SG_HIP(hipEventSynchronize(s.ev[3]));
+        if ((rc = account(s)) != SG_OK) return rc;
+        if ((rc = finish(s)) != SG_OK) return rc;
+        s.busy = false;
+        ++done;
+    }
 }
 
 inline void put_be16(uint8_t* p, uint32_t v) {
@@ -416,11 +463,7 @@ int64_t sg_write_records(sg_ctx* c, uint64_t seq0, uint8_t content_type, uint8_t
     const int ns = record_slots();
     for (int i = 0; i < ns; ++i)
         if ((rc = pipe_streams(c, rs, i, &slot_reset.ps[i])) != SG_OK) return rc;
-    auto any_busy = [&] {
-        for (int i = 0; i < ns; ++i)
-            if (rs->slot[i].busy) return true;
-        return false;
-    };
+    auto streams = [&](const RecordStaging::Slot& s) -> const PipeStreams& { return slot_reset.ps[&s - rs->slot]; };
     size_t wpos = 0;
     // every record but the last is full, so record r starts at r * kWireRec
     constexpr size_t kWireRec = SG_HEADER_LEN + SG_RECORD_MAX_LEN + SG_MAC_LEN;
@@ -429,116 +472,117 @@ int64_t sg_write_records(sg_ctx* c, uint64_t seq0, uint8_t content_type, uint8_t
     // registered caller buffers: DMA straight between them and the device
     const bool zc = zero_copy_enabled() && registered(data, len) && registered(wire, wire_need);
     auto rec_len = [&](uint64_t r) { return (uint32_t)std::min<uint64_t>(SG_RECORD_MAX_LEN, len - r * SG_RECORD_MAX_LEN); };
+    uint64_t next = 0;  // first record of the next chunk to stage
 
-    // frame a drained slot's records into the wire (tls.rs:126-130): the
-    // headers, and (staged path) the fragments from the pinned staging
-    auto emit = [&](RecordStaging::Slot& s) {
+    // host framing copy in, H2D (tls.rs:137-147: 2^14-byte fragments)
+    auto stage = [&](RecordStaging::Slot& s) -> int {
+        const uint32_t k = (uint32_t)std::min<uint64_t>(kChunk, nrec - next);
         const double t0 = now_ms();
-        auto header = [&](uint64_t r) {
-            uint8_t* h = wire + r * kWireRec;
-            h[0] = content_type;
-            h[1] = ver_major;
-            h[2] = ver_minor;
-            put_be16(h + 3, rec_len(r) + SG_MAC_LEN);
-        };
-        if (!zc) {
+        // zero-copy: the chunk's plaintext is contiguous in the caller's buffer
+        // (in_stride 2^14); staged: each record in its 16-byte aligned slot
+        if (zc) {
+            for (uint32_t i = 0; i < k; ++i) s.h_len[i] = rec_len(next + i);
+        } else {
+            int r;
+            if ((r = host_staging(s)) != SG_OK) return r;
+            const uint64_t first = next;
+            copy_run(k, [&](uint32_t i) {
+                const uint64_t rr = first + i;
+                std::memcpy(s.h_in + (size_t)i * kSlot, data + rr * SG_RECORD_MAX_LEN, rec_len(rr));
+                s.h_len[i] = rec_len(rr);
+            });
+        }
+        t_host += now_ms() - t0;
+        bool same = true;  // every record of the chunk has the same length
+        for (uint32_t i = 1; i < k; ++i) same = same && s.h_len[i] == s.h_len[0];
+        const hipStream_t hs = streams(s).h2d;
+        SG_HIP(hipEventRecord(s.ev[0], hs));
+        if (zc) {
+            const size_t bytes = (size_t)(k - 1) * SG_RECORD_MAX_LEN + s.h_len[k - 1];
+            SG_HIP(hipMemcpyAsync(s.d_in, data + next * SG_RECORD_MAX_LEN, bytes, hipMemcpyHostToDevice, hs));
+        } else {
+            SG_HIP(hipMemcpyAsync(s.d_in, s.h_in, (size_t)k * kSlot, hipMemcpyHostToDevice, hs));
+        }
+        if (!same) SG_HIP(hipMemcpyAsync(s.d_len, s.h_len, k * 4u, hipMemcpyHostToDevice, hs));
+        SG_HIP(hipEventRecord(s.ev[1], hs));
+        s.nrec = k;
+        s.first = next;
+        s.zc = zc;
+        next += k;
+        return SG_OK;
+    };
+    // seal (and, zero-copy, the chunk's wire image: headers and fragments,
+    // tls.rs:126-130, built in HBM so that it leaves in one contiguous copy --
+    // a strided copy at the wire's pitch was ~50x slower on the host link)
+    auto launch = [&](RecordStaging::Slot& s) -> int {
+        const uint32_t k = s.nrec;
+        bool same = true;
+        for (uint32_t i = 1; i < k; ++i) same = same && s.h_len[i] == s.h_len[0];
+        const hipStream_t ks = streams(s).krn;
+        sg_batch b;
+        std::memset(&b, 0, sizeof b);
+        b.count = k;
+        b.flags = SG_BATCH_TLS;
+        b.keys = c->d_key;
+        b.num_keys = 1;
+        b.seq0 = seq0 + s.first;
+        b.content_type = content_type;
+        b.ver_major = ver_major;
+        b.ver_minor = ver_minor;
+        b.in = s.d_in;
+        b.in_stride = s.zc ? SG_RECORD_MAX_LEN : kSlot;
+        b.out = s.d_out;
+        b.out_stride = kSlot;
+        // a uniform chunk is a direct launch; a ragged one (the tail) is bucketed
+        b.len = same ? nullptr : s.d_len;
+        b.uniform_len = same ? s.h_len[0] : 0u;
+        b.max_len = SG_RECORD_MAX_LEN;
+        b.stream = ks;
+        b.workspace = s.d_ws;
+        b.workspace_size = sg_workspace_size(kChunk);
+        int r;
+        if ((r = sg_seal_batch(&b)) != SG_OK) return r;
+        if (s.zc) {
+            const uint32_t hdr = content_type | ((uint32_t)ver_major << 8) | ((uint32_t)ver_minor << 16);
+            SG_HIP(launch_frame(s.d_out, kSlot, s.d_wire, (uint32_t)kWireRec, k, SG_RECORD_MAX_LEN + SG_MAC_LEN,
+                                s.h_len[k - 1] + SG_MAC_LEN, hdr, ks));
+        }
+        SG_HIP(hipEventRecord(s.ev[2], ks));
+        return SG_OK;
+    };
+    auto copy_out = [&](RecordStaging::Slot& s) -> int {
+        const uint32_t k = s.nrec, last = s.h_len[k - 1] + SG_MAC_LEN;
+        const hipStream_t ds = streams(s).d2h;
+        if (s.zc) {
+            SG_HIP(hipMemcpyAsync(wire + s.first * kWireRec, s.d_wire, (size_t)(k - 1) * kWireRec + SG_HEADER_LEN + last,
+                                  hipMemcpyDeviceToHost, ds));
+        } else {
+            SG_HIP(hipMemcpyAsync(s.h_out, s.d_out, (size_t)k * kSlot, hipMemcpyDeviceToHost, ds));
+        }
+        SG_HIP(hipEventRecord(s.ev[3], ds));
+        return SG_OK;
+    };
+    // frame the chunk's records into the wire (tls.rs:126-130): the headers and
+    // (staged path) the fragments from the pinned staging
+    auto finish = [&](RecordStaging::Slot& s) -> int {
+        const double t0 = now_ms();
+        if (!s.zc) {
             copy_run(s.nrec, [&](uint32_t i) {
                 const uint64_t r = s.first + i;
-                header(r);
-                std::memcpy(wire + r * kWireRec + SG_HEADER_LEN, s.h_out + (size_t)i * kSlot, rec_len(r) + SG_MAC_LEN);
+                uint8_t* h = wire + r * kWireRec;
+                h[0] = content_type;
+                h[1] = ver_major;
+                h[2] = ver_minor;
+                put_be16(h + 3, rec_len(r) + SG_MAC_LEN);
+                std::memcpy(h + SG_HEADER_LEN, s.h_out + (size_t)i * kSlot, rec_len(r) + SG_MAC_LEN);
             });
         }
         const uint64_t last = s.first + s.nrec - 1;
         wpos = last * kWireRec + SG_HEADER_LEN + (size_t)rec_len(last) + SG_MAC_LEN;
         t_host += now_ms() - t0;
+        return SG_OK;
     };
-
-    uint64_t next = 0;
-    int cur = 0;
-    while (next < nrec || any_busy()) {
-        RecordStaging::Slot& s = rs->slot[cur];
-        if (s.busy) {  // oldest chunk first: keeps the wire in record order
-            if ((rc = drain(s)) != SG_OK) return rc;
-            emit(s);
-        }
-        if (next < nrec) {
-            const uint32_t k = (uint32_t)std::min<uint64_t>(kChunk, nrec - next);
-            const double t0 = now_ms();
-            // zero-copy: the chunk's plaintext is contiguous in the caller's buffer
-            // (in_stride 2^14); staged: each record in its 16-byte aligned slot
-            if (zc) {
-                for (uint32_t i = 0; i < k; ++i) s.h_len[i] = rec_len(next + i);
-            } else {
-                if ((rc = host_staging(s)) != SG_OK) return rc;
-                copy_run(k, [&](uint32_t i) {
-                    const uint64_t r = next + i;
-                    std::memcpy(s.h_in + (size_t)i * kSlot, data + r * SG_RECORD_MAX_LEN, rec_len(r));
-                    s.h_len[i] = rec_len(r);
-                });
-            }
-            bool same = true;  // every record of the chunk has the same length
-            for (uint32_t i = 1; i < k; ++i) same = same && s.h_len[i] == s.h_len[0];
-            t_host += now_ms() - t0;
-            const size_t in_stride = zc ? SG_RECORD_MAX_LEN : kSlot;
-            const PipeStreams& P = slot_reset.ps[cur];
-            hipStream_t hs = P.h2d, ks = P.krn, ds = P.d2h;
-            SG_HIP(hipEventRecord(s.ev[0], hs));
-            if (zc) {
-                const size_t bytes = (size_t)(k - 1) * SG_RECORD_MAX_LEN + s.h_len[k - 1];
-                SG_HIP(hipMemcpyAsync(s.d_in, data + next * SG_RECORD_MAX_LEN, bytes, hipMemcpyHostToDevice, hs));
-            } else {
-                SG_HIP(hipMemcpyAsync(s.d_in, s.h_in, (size_t)k * kSlot, hipMemcpyHostToDevice, hs));
-            }
-            if (!same) SG_HIP(hipMemcpyAsync(s.d_len, s.h_len, k * 4u, hipMemcpyHostToDevice, hs));
-            SG_HIP(hipEventRecord(s.ev[1], hs));
-            if (ks != hs) SG_HIP(hipStreamWaitEvent(ks, s.ev[1], 0));
-            sg_batch b;
-            std::memset(&b, 0, sizeof b);
-            b.count = k;
-            b.flags = SG_BATCH_TLS;
-            b.keys = c->d_key;
-            b.num_keys = 1;
-            b.seq0 = seq0 + next;
-            b.content_type = content_type;
-            b.ver_major = ver_major;
-            b.ver_minor = ver_minor;
-            b.in = s.d_in;
-            b.in_stride = in_stride;
-            b.out = s.d_out;
-            b.out_stride = kSlot;
-            // a uniform chunk is a direct launch; a ragged one (the tail) is bucketed
-            b.len = same ? nullptr : s.d_len;
-            b.uniform_len = same ? s.h_len[0] : 0u;
-            b.max_len = SG_RECORD_MAX_LEN;
-            b.stream = ks;
-            b.workspace = s.d_ws;
-            b.workspace_size = sg_workspace_size(kChunk);
-            if ((rc = sg_seal_batch(&b)) != SG_OK) return rc;
-            const uint32_t last = s.h_len[k - 1] + SG_MAC_LEN;
-            if (zc) {
-                // the chunk's wire image (headers and fragments, tls.rs:126-130) is
-                // built in HBM and leaves in one contiguous copy (a strided copy at
-                // the wire's pitch was ~50x slower on the host link)
-                const uint32_t hdr = content_type | ((uint32_t)ver_major << 8) | ((uint32_t)ver_minor << 16);
-                SG_HIP(launch_frame(s.d_out, kSlot, s.d_wire, (uint32_t)kWireRec, k, SG_RECORD_MAX_LEN + SG_MAC_LEN, last,
-                                    hdr, ks));
-            }
-            SG_HIP(hipEventRecord(s.ev[2], ks));
-            if (ds != ks) SG_HIP(hipStreamWaitEvent(ds, s.ev[2], 0));
-            if (zc) {
-                SG_HIP(hipMemcpyAsync(wire + next * kWireRec, s.d_wire, (size_t)(k - 1) * kWireRec + SG_HEADER_LEN + last,
-                                      hipMemcpyDeviceToHost, ds));
-            } else {
-                SG_HIP(hipMemcpyAsync(s.h_out, s.d_out, (size_t)k * kSlot, hipMemcpyDeviceToHost, ds));
-            }
-            SG_HIP(hipEventRecord(s.ev[3], ds));
-            s.nrec = k;
-            s.first = next;
-            s.busy = true;
-            next += k;
-        }
-        cur = (cur + 1) % ns;
-    }
+    if ((rc = run_pipeline(rs, ns, streams, [&] { return next < nrec; }, stage, launch, copy_out, finish)) != SG_OK) return rc;
     *wire_len = wpos;
     return (int64_t)nrec;
 }
@@ -569,15 +613,6 @@ int sg_read_records(sg_ctx* c, uint64_t seq0, const uint8_t* wire, size_t wire_l
     RecordStaging* rs = nullptr;
     int rc = staging(c, &rs);
     if (rc != SG_OK) return rc;
-    SlotReset slot_reset(rs);
-    const int ns = record_slots();
-    for (int i = 0; i < ns; ++i)
-        if ((rc = pipe_streams(c, rs, i, &slot_reset.ps[i])) != SG_OK) return rc;
-    auto any_busy = [&] {
-        for (int i = 0; i < ns; ++i)
-            if (rs->slot[i].busy) return true;
-        return false;
-    };
 
     const uint64_t nrec = recs.size();
     uint64_t next = 0, good = 0, opos = 0, consumed = 0;
@@ -592,13 +627,33 @@ int sg_read_records(sg_ctx* c, uint64_t seq0, const uint8_t* wire, size_t wire_l
         pre[0] = 0;
         for (uint64_t i = 0; i < nrec; ++i) pre[i + 1] = pre[i] + recs[i].flen - SG_MAC_LEN;
     }
+    // Zero-copy: plaintext DMA'd into `out` beyond the delivered records is
+    // cleared on every exit (the reference releases none of it, tls.rs:268):
+    // collect() clears it chunk by chunk, and an early return (a launch or copy
+    // error) clears everything from the first undelivered record to the end of
+    // the chunks issued.  Declared before the SlotReset, so that it runs after
+    // the pipeline's streams have drained.
+    struct ScrubOut {
+        uint8_t* out;
+        const std::vector<uint64_t>* pre;
+        const uint64_t *good, *next;
+        bool armed;
+        ~ScrubOut() {
+            if (armed && *next > *good) std::memset(out + (*pre)[*good], 0, (*pre)[*next] - (*pre)[*good]);
+        }
+    } scrub{out, &pre, &good, &next, zc};
+    SlotReset slot_reset(rs);
+    const int ns = record_slots();
+    for (int i = 0; i < ns; ++i)
+        if ((rc = pipe_streams(c, rs, i, &slot_reset.ps[i])) != SG_OK) return rc;
+    auto streams = [&](const RecordStaging::Slot& s) -> const PipeStreams& { return slot_reset.ps[&s - rs->slot]; };
+
     std::vector<uint64_t> dst_off(kChunk);
-    std::vector<uint8_t> chunk_zc(kMaxSlots, 0);  // per slot: the chunk went the zero-copy way
-    auto collect = [&](RecordStaging::Slot& s, bool szc) {
+    auto collect = [&](RecordStaging::Slot& s) -> int {
         const double t0 = now_ms();
         if (error != SG_OK) {  // stopped earlier: nothing of this chunk is delivered
-            if (szc) std::memset(out + pre[s.first], 0, pre[s.first + s.nrec] - pre[s.first]);
-            return;
+            if (s.zc) std::memset(out + pre[s.first], 0, pre[s.first + s.nrec] - pre[s.first]);
+            return SG_OK;
         }
         // the records up to the first failing one are delivered (tls.rs:268: the
         // reader stops at its first Err); their output offsets are a prefix sum
@@ -613,7 +668,7 @@ int sg_read_records(sg_ctx* c, uint64_t seq0, const uint8_t* wire, size_t wire_l
             opos += R.flen - SG_MAC_LEN;
             consumed += SG_HEADER_LEN + R.flen;
         }
-        if (szc) {
+        if (s.zc) {
             // the plaintext is in place already; from a failed record on, the
             // DMA'd bytes are cleared (the reference releases none of them)
             if (ok < s.nrec) std::memset(out + pre[s.first + ok], 0, pre[s.first + s.nrec] - pre[s.first + ok]);
@@ -634,126 +689,138 @@ int sg_read_records(sg_ctx* c, uint64_t seq0, const uint8_t* wire, size_t wire_l
         }
         good += ok;
         t_host += now_ms() - t0;
+        return SG_OK;
     };
 
-    int cur = 0;
-    while (next < nrec || any_busy()) {
-        RecordStaging::Slot& s = rs->slot[cur];
-        if (s.busy) {
-            if ((rc = drain(s)) != SG_OK) return rc;
-            collect(s, chunk_zc[cur] != 0);
+    // host framing copy in (staged) and the H2D of the fragments or wire image
+    auto stage = [&](RecordStaging::Slot& s) -> int {
+        const uint32_t k = (uint32_t)std::min<uint64_t>(kChunk, nrec - next);
+        const double t0 = now_ms();
+        const Rec& R0 = recs[next];
+        bool same = true, tls = true, dense = true;
+        for (uint32_t i = 0; i < k; ++i) {
+            const Rec& R = recs[next + i];
+            same = same && R.flen == R0.flen;
+            tls = tls && R.type == R0.type && R.major == R0.major && R.minor == R0.minor;
+            dense = dense && R.off == R0.off + (size_t)i * (SG_HEADER_LEN + R0.flen);
         }
-        if (next < nrec && error == SG_OK) {
-            const uint32_t k = (uint32_t)std::min<uint64_t>(kChunk, nrec - next);
-            const double t0 = now_ms();
-            const Rec& R0 = recs[next];
-            bool same = true, tls = true, dense = true;
+        // zero-copy for chunks of equal, back-to-back records (a stream of
+        // full records); any other chunk goes through the staging
+        s.zc = zc && same && dense;
+        if (!s.zc) {
+            int r;
+            if ((r = host_staging(s)) != SG_OK) return r;
+            const uint64_t first = next;
+            copy_run(k, [&](uint32_t i) {
+                const Rec& R = recs[first + i];
+                std::memcpy(s.h_in + (size_t)i * kSlot, wire + R.off, R.flen);
+                s.h_len[i] = R.flen;
+            });
+        }
+        // TLS mode (nonce and AD built on the device, tls.rs:250-265) when the
+        // chunk's records share type and version; else explicit nonce / AD
+        if (!tls) {
             for (uint32_t i = 0; i < k; ++i) {
                 const Rec& R = recs[next + i];
-                same = same && R.flen == R0.flen;
-                tls = tls && R.type == R0.type && R.major == R0.major && R.minor == R0.minor;
-                dense = dense && R.off == R0.off + (size_t)i * (SG_HEADER_LEN + R0.flen);
+                const uint64_t seq = seq0 + next + i;
+                // nonce = be64(seq) (tls.rs:250); AD = seq || type || major || minor ||
+                // be16(len - 16) (tls.rs:252-265).  Layout: nonces[kChunk][8], ads[kChunk][13]
+                put_be64(s.h_meta + 8u * i, seq);
+                uint8_t* m = s.h_meta + 8u * kChunk + 13u * i;
+                put_be64(m, seq);
+                m[8] = R.type;
+                m[9] = R.major;
+                m[10] = R.minor;
+                put_be16(m + 11, R.flen - SG_MAC_LEN);
             }
-            // zero-copy for chunks of equal, back-to-back records (a stream of
-            // full records); any other chunk goes through the staging
-            const bool czc = zc && same && dense;
-            chunk_zc[cur] = czc ? 1 : 0;
-            // TLS mode (nonce and AD built on the device, tls.rs:250-265) when the
-            // chunk's records share type and version; else explicit nonce / AD
-            if (!czc) {
-                if ((rc = host_staging(s)) != SG_OK) return rc;
-                copy_run(k, [&](uint32_t i) {
-                    const Rec& R = recs[next + i];
-                    std::memcpy(s.h_in + (size_t)i * kSlot, wire + R.off, R.flen);
-                    s.h_len[i] = R.flen;
-                });
-            }
-            if (!tls) {
-                for (uint32_t i = 0; i < k; ++i) {
-                    const Rec& R = recs[next + i];
-                    const uint64_t seq = seq0 + next + i;
-                    // nonce = be64(seq) (tls.rs:250); AD = seq || type || major || minor ||
-                    // be16(len - 16) (tls.rs:252-265).  Layout: nonces[kChunk][8], ads[kChunk][13]
-                    put_be64(s.h_meta + 8u * i, seq);
-                    uint8_t* m = s.h_meta + 8u * kChunk + 13u * i;
-                    put_be64(m, seq);
-                    m[8] = R.type;
-                    m[9] = R.major;
-                    m[10] = R.minor;
-                    put_be16(m + 11, R.flen - SG_MAC_LEN);
-                }
-            }
-            t_host += now_ms() - t0;
-            const PipeStreams& P = slot_reset.ps[cur];
-            hipStream_t hs = P.h2d, ks = P.krn, ds = P.d2h;
-            SG_HIP(hipEventRecord(s.ev[0], hs));
-            const uint32_t pitch = SG_HEADER_LEN + R0.flen;
-            if (czc) {  // the chunk's wire image in one contiguous copy, taken apart in HBM
-                SG_HIP(hipMemcpyAsync(s.d_wire, wire + R0.off - SG_HEADER_LEN, (size_t)k * pitch, hipMemcpyHostToDevice,
-                                      hs));
-            } else {
-                SG_HIP(hipMemcpyAsync(s.d_in, s.h_in, (size_t)k * kSlot, hipMemcpyHostToDevice, hs));
-                if (!same) SG_HIP(hipMemcpyAsync(s.d_len, s.h_len, k * 4u, hipMemcpyHostToDevice, hs));
-            }
-            if (!tls) {
-                SG_HIP(hipMemcpyAsync(s.d_meta, s.h_meta, 8u * k, hipMemcpyHostToDevice, hs));
-                SG_HIP(hipMemcpyAsync(s.d_meta + 8u * kChunk, s.h_meta + 8u * kChunk, 13u * k, hipMemcpyHostToDevice,
-                                      hs));
-            }
-            SG_HIP(hipEventRecord(s.ev[1], hs));
-            if (ks != hs) SG_HIP(hipStreamWaitEvent(ks, s.ev[1], 0));
-            if (czc) SG_HIP(launch_unframe(s.d_wire, pitch, s.d_in, kSlot, k, R0.flen, ks));
-            sg_batch b;
-            std::memset(&b, 0, sizeof b);
-            b.count = k;
-            b.keys = c->d_key;
-            b.num_keys = 1;
-            if (tls) {
-                b.flags = SG_BATCH_TLS;
-                b.seq0 = seq0 + next;
-                b.content_type = R0.type;
-                b.ver_major = R0.major;
-                b.ver_minor = R0.minor;
-            } else {
-                b.nonces = s.d_meta;
-                b.ads = s.d_meta + 8u * kChunk;
-                b.ad_len = 13;
-                b.ad_stride = 13;
-            }
-            b.in = s.d_in;
-            b.in_stride = kSlot;
-            b.out = s.d_out;
-            // zero-copy: plaintext back to back, as it lands in `out`
-            b.out_stride = czc ? (size_t)(R0.flen - SG_MAC_LEN) : kSlot;
-            b.len = same ? nullptr : s.d_len;
-            b.uniform_len = same ? R0.flen : 0u;
-            b.max_len = SG_ENC_RECORD_MAX_LEN;
-            b.status = s.d_status;
-            b.stream = ks;
-            b.workspace = s.d_ws;
-            b.workspace_size = sg_workspace_size(kChunk);
-            // staged: the reader delivers nothing from a failed record (it stops
-            // there), so no device scrub of failed records' output; zero-copy: the
-            // output goes to the caller's memory by DMA, so failed records are
-            // scrubbed on the device first
-            if (!czc) b.flags |= SG_BATCH_KEEP_FAILED;
-            if ((rc = sg_open_batch(&b)) != SG_OK) return rc;
-            SG_HIP(hipEventRecord(s.ev[2], ks));
-            if (ds != ks) SG_HIP(hipStreamWaitEvent(ds, s.ev[2], 0));
-            if (czc) {
-                SG_HIP(hipMemcpyAsync(out + pre[next], s.d_out, pre[next + k] - pre[next], hipMemcpyDeviceToHost, ds));
-            } else {
-                SG_HIP(hipMemcpyAsync(s.h_out, s.d_out, (size_t)k * kSlot, hipMemcpyDeviceToHost, ds));
-            }
-            SG_HIP(hipMemcpyAsync(s.h_status, s.d_status, k, hipMemcpyDeviceToHost, ds));
-            SG_HIP(hipEventRecord(s.ev[3], ds));
-            s.nrec = k;
-            s.first = next;
-            s.busy = true;
-            next += k;
         }
-        cur = (cur + 1) % ns;
-    }
+        t_host += now_ms() - t0;
+        const hipStream_t hs = streams(s).h2d;
+        SG_HIP(hipEventRecord(s.ev[0], hs));
+        if (s.zc) {  // the chunk's wire image in one contiguous copy, taken apart in HBM
+            SG_HIP(hipMemcpyAsync(s.d_wire, wire + R0.off - SG_HEADER_LEN, (size_t)k * (SG_HEADER_LEN + R0.flen),
+                                  hipMemcpyHostToDevice, hs));
+        } else {
+            SG_HIP(hipMemcpyAsync(s.d_in, s.h_in, (size_t)k * kSlot, hipMemcpyHostToDevice, hs));
+            if (!same) SG_HIP(hipMemcpyAsync(s.d_len, s.h_len, k * 4u, hipMemcpyHostToDevice, hs));
+        }
+        if (!tls) {
+            SG_HIP(hipMemcpyAsync(s.d_meta, s.h_meta, 8u * k, hipMemcpyHostToDevice, hs));
+            SG_HIP(hipMemcpyAsync(s.d_meta + 8u * kChunk, s.h_meta + 8u * kChunk, 13u * k, hipMemcpyHostToDevice, hs));
+        }
+        SG_HIP(hipEventRecord(s.ev[1], hs));
+        s.nrec = k;
+        s.first = next;
+        next += k;
+        return SG_OK;
+    };
+    auto launch = [&](RecordStaging::Slot& s) -> int {
+        const uint32_t k = s.nrec;
+        const Rec& R0 = recs[s.first];
+        bool same = true, tls = true;
+        for (uint32_t i = 0; i < k; ++i) {
+            const Rec& R = recs[s.first + i];
+            same = same && R.flen == R0.flen;
+            tls = tls && R.type == R0.type && R.major == R0.major && R.minor == R0.minor;
+        }
+        const hipStream_t ks = streams(s).krn;
+        if (s.zc) SG_HIP(launch_unframe(s.d_wire, SG_HEADER_LEN + R0.flen, s.d_in, kSlot, k, R0.flen, ks));
+        sg_batch b;
+        std::memset(&b, 0, sizeof b);
+        b.count = k;
+        b.keys = c->d_key;
+        b.num_keys = 1;
+        if (tls) {
+            b.flags = SG_BATCH_TLS;
+            b.seq0 = seq0 + s.first;
+            b.content_type = R0.type;
+            b.ver_major = R0.major;
+            b.ver_minor = R0.minor;
+        } else {
+            b.nonces = s.d_meta;
+            b.ads = s.d_meta + 8u * kChunk;
+            b.ad_len = 13;
+            b.ad_stride = 13;
+        }
+        b.in = s.d_in;
+        b.in_stride = kSlot;
+        b.out = s.d_out;
+        // zero-copy: plaintext back to back, as it lands in `out`
+        b.out_stride = s.zc ? (size_t)(R0.flen - SG_MAC_LEN) : kSlot;
+        b.len = same ? nullptr : s.d_len;
+        b.uniform_len = same ? R0.flen : 0u;
+        b.max_len = SG_ENC_RECORD_MAX_LEN;
+        b.status = s.d_status;
+        b.stream = ks;
+        b.workspace = s.d_ws;
+        b.workspace_size = sg_workspace_size(kChunk);
+        // staged: the reader delivers nothing from a failed record (it stops
+        // there), so no device scrub of failed records' output; zero-copy: the
+        // output goes to the caller's memory by DMA, so failed records are
+        // scrubbed on the device first
+        if (!s.zc) b.flags |= SG_BATCH_KEEP_FAILED;
+        int r;
+        if ((r = sg_open_batch(&b)) != SG_OK) return r;
+        SG_HIP(hipEventRecord(s.ev[2], ks));
+        return SG_OK;
+    };
+    auto copy_out = [&](RecordStaging::Slot& s) -> int {
+        const uint32_t k = s.nrec;
+        const hipStream_t ds = streams(s).d2h;
+        if (s.zc) {
+            SG_HIP(hipMemcpyAsync(out + pre[s.first], s.d_out, pre[s.first + k] - pre[s.first], hipMemcpyDeviceToHost,
+                                  ds));
+        } else {
+            SG_HIP(hipMemcpyAsync(s.h_out, s.d_out, (size_t)k * kSlot, hipMemcpyDeviceToHost, ds));
+        }
+        SG_HIP(hipMemcpyAsync(s.h_status, s.d_status, k, hipMemcpyDeviceToHost, ds));
+        SG_HIP(hipEventRecord(s.ev[3], ds));
+        return SG_OK;
+    };
+    if ((rc = run_pipeline(rs, ns, streams, [&] { return next < nrec && error == SG_OK; }, stage, launch, copy_out, collect)) !=
+        SG_OK)
+        return rc;
+    scrub.armed = false;  // collect() has cleared whatever it did not deliver
     res->records = good;
     res->consumed = consumed;
     res->out_len = opos;

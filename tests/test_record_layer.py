@@ -358,6 +358,62 @@ def test_gpu_zero_copy_record_path(gpu, oracle):
 
 
 @pytest.mark.gpu
+def test_gpu_zero_copy_odd_length_records(gpu, oracle):
+    """Registered-buffer read of 600 equal records of an odd plaintext length
+    (1001 B: the open batch writes the plaintext back to back at a packed,
+    unaligned 1001-byte stride, i.e. the byte-granular output and scrub paths,
+    advisor r5).  `out` equals the staged path's and the input; with a
+    corrupted record in the first chunk and, separately, one in the second,
+    the records before it are delivered and every byte of `out` from it on is
+    zero (tls.rs:268: nothing of a failed record or of any record after it)."""
+    import ctypes as C
+
+    import numpy as np
+
+    from suruga_amd import ChaCha20Poly1305
+    from suruga_amd import _native as N
+
+    lib = N.load()
+    key = bytes(range(11, 43))
+    n, count, seq0 = 1001, 600, 9
+    data = np.frombuffer(oracle.fill_record(0x3C, 5, n * count), dtype=np.uint8).copy()
+    pitch = 5 + n + 16
+    wire = np.zeros(pitch * count, dtype=np.uint8)
+    for r in range(count):
+        ct = oracle.seal(key, struct.pack(">Q", seq0 + r), data[r * n:(r + 1) * n].tobytes(), oracle.tls_ad(seq0 + r, n))
+        wire[r * pitch:(r + 1) * pitch] = np.frombuffer(bytes([23, 3, 3]) + struct.pack(">H", n + 16) + ct,
+                                                       dtype=np.uint8)
+    dec = ChaCha20Poly1305().new_decryptor(key)
+    res = N.SgReadResult()
+
+    def read(w, out):
+        N.check(lib.sg_read_records(dec._ptr, seq0, w.ctypes.data, w.size, out.ctypes.data, out.size, None, None,
+                                    1 << 20, C.byref(res)))
+        return res.records, res.out_len, res.error
+
+    staged = np.full(n * count, 0xEE, dtype=np.uint8)
+    assert read(wire.copy(), staged) == (count, n * count, N.SG_OK)
+    assert np.array_equal(staged, data)
+    out = np.full(n * count, 0xEE, dtype=np.uint8)
+    for a in (wire, out):
+        N.check(lib.sg_host_register(a.ctypes.data, a.nbytes))
+    try:
+        assert read(wire, out) == (count, n * count, N.SG_OK)
+        assert np.array_equal(out, staged)
+        for bad, pos in ((100, 7), (300, n - 1)):  # first chunk; second chunk, the last byte
+            w = wire[bad * pitch + 5 + pos]
+            wire[bad * pitch + 5 + pos] ^= 0x01
+            out[:] = 0xEE
+            assert read(wire, out) == (bad, bad * n, N.SG_E_BAD_MAC)
+            assert np.array_equal(out[:bad * n], data[:bad * n])
+            assert not out[bad * n:].any(), f"bytes of undelivered records left in out (bad record {bad})"
+            wire[bad * pitch + 5 + pos] = w
+    finally:
+        for a in (wire, out):
+            N.check(lib.sg_host_unregister(a.ctypes.data))
+
+
+@pytest.mark.gpu
 def test_gpu_zero_copy_edges(gpu, oracle):
     """Registered-buffer edges: a write shorter than one record, and a read
     whose second chunk mixes content types (equal, back-to-back fragments: the

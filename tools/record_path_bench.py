@@ -1,13 +1,18 @@
 #!/usr/bin/env python3
-"""Copy-inclusive rate of the GPU record path, one direction at a time (C4's
-host side, tls.rs:126-130 write / :238-281 read).
+"""Copy-inclusive rate of the GPU record path, one direction at a time and
+both at once (C4's host side, tls.rs:126-130 write / :238-281 read).
 
 Writer: sg_write_records over a host buffer of application data (fragment into
 2^14-byte records, pinned staging, H2D, seal, D2H, 5-byte headers) into a host
 wire buffer.  Reader: sg_read_records over that wire back into a host buffer.
 Both are timed wall-clock around the calls, from and to pageable host memory,
 so every copy is inside the number.  The read-back is compared with the input
-byte for byte.  Prints one JSON line (and writes it with --json-out): GiB/s of
+byte for byte.  Duplex (round 6): a writer and a reader on two contexts and
+two threads at once -- the writer seals the stream again into a second wire
+buffer while the reader opens the first, as suruga's client runs its reader and
+writer independently over a cloned socket (client.rs:19-24, 269-271) -- timed
+wall-clock around both; `duplex_gibs` counts the bytes of both directions and
+both outputs are checked.  Prints one JSON line (and writes it with --json-out): GiB/s of
 application data per direction plus the per-GiB split of H2D, kernel, D2H and
 host framing time (sg_record_timing) for SG_COPY_THREADS = each --threads value.
 
@@ -40,11 +45,12 @@ def one(total: int, call: int, device: int, registered: bool = False) -> dict:
     lib = N.load()
     data = np.random.default_rng(0xC4).integers(0, 256, size=total, dtype=np.uint8)
     wire = np.empty(lib.sg_wire_bound(total), dtype=np.uint8)
+    wire2 = np.empty_like(wire)
     back = np.empty(total, dtype=np.uint8)
     aead = ChaCha20Poly1305(device)
     enc, dec = aead.new_encryptor(KEY), aead.new_decryptor(KEY)
     if registered:  # the zero-copy path: DMA straight between these buffers and the device
-        for a in (data, wire, back):
+        for a in (data, wire, wire2, back):
             N.check(lib.sg_host_register(a.ctypes.data, a.nbytes))
 
     def timing(acc):
@@ -53,13 +59,13 @@ def one(total: int, call: int, device: int, registered: bool = False) -> dict:
         for k, x in zip(("h2d", "kernel", "d2h", "host"), v):
             acc[k] = acc.get(k, 0.0) + x.value
 
-    def write_all(acc):
+    def write_all(acc, dst=wire):
         wl = C.c_size_t(0)
         seq, pos, wpos = 0, 0, 0
         while pos < total:
             n = min(call, total - pos)
             seq += N.check(lib.sg_write_records(enc._ptr, seq, 23, 3, 3, C.c_void_p(data.ctypes.data + pos), n,
-                                                C.c_void_p(wire.ctypes.data + wpos), wire.size - wpos,
+                                                C.c_void_p(dst.ctypes.data + wpos), dst.size - wpos,
                                                 C.byref(wl)))
             if acc is not None:
                 timing(acc)
@@ -94,14 +100,43 @@ def one(total: int, call: int, device: int, registered: bool = False) -> dict:
     rrec, olen = read_all(wlen, racc)
     tr = time.perf_counter() - t0
     ok = rrec == nrec and olen == total and bool(np.array_equal(back, data))
+    # duplex: the writer into wire2 and the reader from wire, two threads (ctypes
+    # releases the GIL for the calls)
+    import threading
+
+    back[:] = 0
+    stamps, errs = {}, []
+
+    def timed(name, fn):
+        try:
+            t0 = time.perf_counter()
+            fn()
+            stamps[name] = time.perf_counter() - t0
+        except Exception as e:  # reported below
+            errs.append(repr(e))
+
+    ths = [threading.Thread(target=timed, args=("write", lambda: write_all(None, wire2))),
+           threading.Thread(target=timed, args=("read", lambda: read_all(wlen, None)))]
+    t0 = time.perf_counter()
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    td = time.perf_counter() - t0
+    dok = not errs and bool(np.array_equal(back, data)) and bool(np.array_equal(wire2[:wlen], wire[:wlen]))
     if registered:
-        for a in (data, wire, back):
+        for a in (data, wire, wire2, back):
             N.check(lib.sg_host_unregister(a.ctypes.data))
     gib = total / 2**30
     per = lambda acc: {k + "_ms_per_gib": round(v / gib, 2) for k, v in acc.items()}  # noqa: E731
     return {"write_gibs": round(gib / tw, 3), "read_gibs": round(gib / tr, 3), "write_ms": round(tw * 1e3, 1),
             "read_ms": round(tr * 1e3, 1), "records": nrec, "correct": ok, "write_split": per(wacc),
-            "read_split": per(racc), "registered": registered}
+            "read_split": per(racc), "registered": registered,
+            "duplex": {"gibs": round(2 * gib / td, 3), "ms": round(td * 1e3, 1),
+                       "write_ms": round(stamps.get("write", 0) * 1e3, 1),
+                       "read_ms": round(stamps.get("read", 0) * 1e3, 1),
+                       "vs_slower_single": round((2 * gib / td) / min(gib / tw, gib / tr), 3),
+                       "vs_serial": round((tw + tr) / td, 3), "correct": dok, "errors": errs}}
 
 
 def main():
@@ -138,10 +173,11 @@ def main():
     lib = N.load()
     out = {"config": f"C4 host side: {a.bytes} B application data, {a.call_bytes} B per sg_write_records call, "
                      "pageable host buffers (\"+registered\": registered with sg_host_register, the zero-copy path), "
-                     "one direction at a time, wall clock around the calls",
+                     "one direction at a time (write_gibs, read_gibs) and both at once on two contexts and threads "
+                     "(duplex.gibs: both directions' bytes over the wall time), wall clock around the calls",
            "kernels": lib.sg_build_info().decode(), "library": N.loaded_info(),
            "host_cpus": len(os.sched_getaffinity(0)), "by_copy_threads": runs,
-           "correct": all(r["correct"] for r in runs.values())}
+           "correct": all(r["correct"] and r["duplex"]["correct"] for r in runs.values())}
     print(json.dumps(out))
     if a.json_out:
         Path(a.json_out).write_text(json.dumps(out, indent=1) + "\n")
