@@ -70,6 +70,9 @@ def parse():
                     help="C1 runs: timed steps of the C2 sub-record appended to the line (0 = none)")
     ap.add_argument("--energy-seconds", type=float, default=2.0,
                     help="length of the energy window after the event-timed steps (0 = no energy fields)")
+    ap.add_argument("--record-path-bytes", type=int, default=1 << 30,
+                    help="C4 host side after the device-resident lines: sg_write_records / sg_read_records over "
+                         "this many application bytes from host memory (0: skip; rank 0 at N=1 only)")
     ap.add_argument("--traffic", default=None,
                     help="PMC-derived HBM traffic summary (tools/pmc_traffic.py)")
     return ap.parse_args()
@@ -304,6 +307,63 @@ def bitexact_check_c2(lay, pt, ct, seq_off):
         ok = ok and ct[q:q + n + 16].cpu().numpy().tobytes() == exp
     return {"bitexact_fold": fold == ref_fold, "fold_records": count, "bitexact_sample": ok,
             "sample_records": len(sample), "oracle_fold_s": round(fold_s, 2)}
+
+
+def measure_record_path(args, bus):
+    """The copy-inclusive rate (north star: "the rate including hipMemcpy to and
+    from the GPU"; BASELINE.json configs[4]'s host side): sg_write_records /
+    sg_read_records over --record-path-bytes of application data in host
+    memory, 64 MiB per call, one direction at a time and both at once (writer
+    and reader on two contexts and threads), from pageable buffers (the staged
+    path) and from buffers registered with sg_host_register (zero-copy), wall
+    clock around the calls, with the H2D / kernel / D2H / host-framing split
+    per GiB (tools/record_path_bench.py).  Every byte read back is compared
+    with the input, the duplex wire with the single-direction one, and a
+    sample of the written records (first, every 4099th, last) with the
+    oracle's TLS sealing of the same bytes (checker only).  Never `value`."""
+    import struct
+
+    import numpy as np
+
+    sys.path.insert(0, str(ROOT / "tests"))
+    sys.path.insert(0, str(ROOT / "tools"))
+    from oracle_ffi import oracle as get_oracle  # checker only
+    from record_path_bench import one
+
+    o = get_oracle()
+    rec = 16384
+    wrec = 5 + rec + 16
+    # on the CPUs of the card's NUMA node from here on (host buffers first
+    # touched below, the copy threads created by the first record call)
+    from suruga_amd import devmon
+
+    prev = os.sched_getaffinity(0)
+    cpus, how = devmon.pin_to_gpu_node(bus)
+
+    def check_wire(data, wire, wlen):
+        nrec = -(-data.size // rec)
+        for r in sorted(set([0, nrec // 2, nrec - 1] + list(range(0, nrec, 4099)))):
+            n = min(rec, data.size - r * rec)
+            hdr = bytes([23, 3, 3]) + struct.pack(">H", n + 16)
+            exp = hdr + o.seal(KEY, struct.pack(">Q", r), data[r * rec:r * rec + n].tobytes(), o.tls_ad(r, n))
+            if wire[r * wrec:r * wrec + 5 + n + 16].tobytes() != exp:
+                return False
+        return True
+
+    total = args.record_path_bytes
+    data = np.frombuffer(np.random.default_rng(0xC4).bytes(total), dtype=np.uint8).copy()
+    runs = {}
+    t0 = time.perf_counter()
+    for reg in (False, True):
+        runs["registered" if reg else "pageable"] = one(total, 64 << 20, 0, reg, check_wire, data)
+    out = {"bytes": total, "call_bytes": 64 << 20, "copy_threads": int(os.environ.get("SG_COPY_THREADS", "8")),
+           "note": "application GiB/s per direction from host memory, every copy inside; duplex.gibs counts both "
+                   "directions' bytes; one key, seq from 0, content type 23, TLS 1.2 (tls.rs:126-130, 238-281)",
+           **runs, "wall_s": round(time.perf_counter() - t0, 1)}
+    out["correct"] = all(r["correct"] and r["duplex"]["correct"] and r["wire_sample_ok"] for r in runs.values())
+    out["pinned"] = {"cpus": len(cpus) if cpus else None, "how": how}
+    os.sched_setaffinity(0, prev)
+    return out
 
 
 def measure_scatter_gather(args, dist, backend, rank, world, dev, n, count, seq0, seal_b, lib, keys, ws, stream):
@@ -976,6 +1036,17 @@ def main():
               "ranks": r2["ranks"], **{kk: vv for kk, vv in (r2["exact"] or {}).items()},
               **{kk: vv for kk, vv in r2["flags"].items() if vv is not None}}
         correct = correct and r2["correct"]
+        del w2
+        torch.cuda.empty_cache()
+    # the copy-inclusive rate of the record path: a side
+    # measurement after the device-resident lines; its correctness joins the line's
+    record_path = None
+    if rank == 0 and world == 1 and args.record_path_bytes > 0:
+        try:
+            record_path = measure_record_path(args, bus)
+            correct = correct and record_path["correct"]
+        except (RuntimeError, OSError, ValueError) as e:
+            record_path = {"error": f"{type(e).__name__}: {e}"[:300]}
     sampler.stop()
     if rank == 0:
         line = {
@@ -1001,6 +1072,8 @@ def main():
             line["scatter_gather"] = scatter_gather
         if c2 is not None:
             line["c2"] = c2
+        if record_path is not None:
+            line["record_path"] = record_path
         print(json.dumps(line), flush=True)
     if dist:
         dist.barrier()

@@ -21,6 +21,7 @@
 #include <functional>
 #include <thread>
 #include <vector>
+#include <immintrin.h>
 
 #include "../../include/suruga_gpu.h"
 #include "sg_host.h"
@@ -33,7 +34,7 @@ namespace {
 constexpr uint32_t kChunk = 256;                                  // records per pipeline chunk
 constexpr uint32_t kSlot = ((SG_ENC_RECORD_MAX_LEN + 63u) / 64u) * 64u;  // device bytes per record
 constexpr uint32_t kMetaBytes = 8u + 13u;                         // nonce + AD per record (reader)
-constexpr int kMaxSlots = 3;                                      // pipeline depth (record_slots)
+constexpr int kMaxSlots = 8;                                      // pipeline depth (record_slots)
 
 thread_local double t_h2d = 0, t_kernel = 0, t_d2h = 0, t_host = 0;
 
@@ -158,36 +159,36 @@ struct RecordStaging {
         bool zc = false;         // the chunk goes the zero-copy way
         bool busy = false;
     } slot[kMaxSlots];
+    hipStream_t krn = nullptr;  // the context's kernel stream (copy-stream mode 1)
 };
 
-// Pipeline depth.  Three slots (default) keep one chunk's H2D, another's
-// kernels and a third's D2H in flight at once: with two, a chunk's D2H waited
-// for its own kernels while the next chunk's H2D was already done.
-// SG_RECORD_SLOTS=2 gives the round-4 two-slot pipeline (A/B).
+// Pipeline depth (SG_RECORD_SLOTS, 2..8).  Four slots (default since round 6)
+// keep a chunk's H2D, another's kernels and a third's D2H in flight while the
+// host-gated pipeline (run_pipeline) notices each step's end: round 5's three
+// slots were enough for the device-waited form, where a chunk's whole chain was
+// enqueued at once.
 int record_slots() {
     static const int n = [] {
         const char* e = std::getenv("SG_RECORD_SLOTS");
-        const int v = e ? std::atoi(e) : kMaxSlots;
+        const int v = e ? std::atoi(e) : 4;
         return v < 2 ? 2 : (v > kMaxSlots ? kMaxSlots : v);
     }();
     return n;
 }
 
 // Stream layout.  Mode 1 (default): the host-link copies of every context on
-// one process-wide stream per direction and each context's kernels on its
-// slot-0 stream, so that one slot's H2D runs beside another's kernels and a
-// third's D2H, the copies on different DMA engines while the process stays
-// within a few hardware queues (GPU_MAX_HW_QUEUES = 4: more streams than that
-// share queues and serialise).  Same box, 1 GiB per direction, 8 copy threads
-// (profiles/r05g): registered buffers 17.4 -> 27.6 GiB/s write, 23.4 -> 25.8
-// read; pageable 12.6 -> 15.2 write, 15.8 -> 14.5 read.  Round 6 measured the
-// alternatives for a reader and a writer at once (profiles/r06d): the D2H on a
-// stream of each context's own (the context's spare slot stream) 14.8 instead
-// of 29.7 GiB/s registered read, both copy directions per context 24.2 instead
-// of 31.7 write -- the extra streams share hardware queues -- while with the
-// shared copy streams the two directions at once run 1.06-1.34x faster than one
-// after the other.  Mode 0 (SG_COPY_STREAMS=0): each slot's copies and kernels
-// on the slot's stream.
+// one process-wide stream per direction and each context's kernels on a stream
+// of its own, so that one slot's H2D runs beside another's kernels and a
+// third's D2H, the copies on different DMA engines, while a reader and a writer
+// use four streams in all -- within the process's hardware queues
+// (GPU_MAX_HW_QUEUES = 4: more streams than that share queues and serialise).
+// Round 5, same box, 1 GiB per direction, 8 copy threads (profiles/r05g):
+// registered buffers 17.4 -> 27.6 GiB/s write, 23.4 -> 25.8 read against
+// per-slot streams; pageable 12.6 -> 15.2 write, 15.8 -> 14.5 read.  Round 6
+// (profiles/r06/, r06d): the D2H on a stream of each context's own 14.8
+// instead of 29.7 GiB/s registered read, both copy directions per context 24.2
+// instead of 31.7 write -- the extra streams share hardware queues.  Mode 0
+// (SG_COPY_STREAMS=0): each slot's copies and kernels on the slot's stream.
 struct PipeStreams {
     hipStream_t h2d, krn, d2h;
 };
@@ -218,6 +219,10 @@ hipError_t process_copy_streams(int dev, hipStream_t* h2d, hipStream_t* d2h) {
 void record_staging_free(RecordStaging* rs) {
     if (!rs) return;
 
+    if (rs->krn) {
+        (void)hipStreamSynchronize(rs->krn);
+        (void)hipStreamDestroy(rs->krn);
+    }
     for (auto& s : rs->slot) {
         if (s.st) (void)hipStreamSynchronize(s.st);
         (void)hipHostFree(s.h_in);
@@ -246,6 +251,19 @@ int staging(sg_ctx* c, RecordStaging** out) {
         auto* rs = new RecordStaging();
         c->rec = rs;  // freed with the context even if allocation below fails
         const size_t bytes = (size_t)kChunk * kSlot;
+        // Mode 1: the process's copy streams first, then the context's kernel
+        // stream, and no stream that the pipeline does not use: HIP hands a
+        // process's streams its hardware queues round-robin (GPU_MAX_HW_QUEUES =
+        // 4), and a kernel stream that shares a queue with the D2H stream runs
+        // its kernels behind the copies (round 6: the standalone write at 22.3
+        // GiB/s registered with the kernels on a context stream created before
+        // the copy streams, r06l, against 35.1 in a process whose other
+        // streams happened to separate them)
+        if (copy_streams_mode() != 0) {
+            hipStream_t h = nullptr, d = nullptr;
+            SG_HIP(process_copy_streams(c->device, &h, &d));
+            SG_HIP(hipStreamCreateWithFlags(&rs->krn, hipStreamNonBlocking));
+        }
         for (int i = 0; i < record_slots(); ++i) {  // (h_in / h_out: host_staging, on first use)
             auto& s = rs->slot[i];
             SG_HIP(hipHostMalloc((void**)&s.h_meta, (size_t)kChunk * kMetaBytes, hipHostMallocDefault));
@@ -258,7 +276,7 @@ int staging(sg_ctx* c, RecordStaging** out) {
             SG_HIP(hipMalloc((void**)&s.d_status, kChunk));
             SG_HIP(hipMalloc((void**)&s.d_len, kChunk * 4u));
             SG_HIP(hipMalloc(&s.d_ws, sg_workspace_size(kChunk)));
-            SG_HIP(hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking));
+            if (copy_streams_mode() == 0) SG_HIP(hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking));
             for (auto& e : s.ev) SG_HIP(hipEventCreate(&e));
         }
     }
@@ -320,7 +338,7 @@ int pipe_streams(sg_ctx* c, RecordStaging* rs, int i, PipeStreams* out) {
     }
     hipStream_t h = nullptr, d = nullptr;
     SG_HIP(process_copy_streams(c->device, &h, &d));
-    *out = {h, rs->slot[0].st, d};
+    *out = {h, rs->krn, d};
     return SG_OK;
 }
 
@@ -338,32 +356,113 @@ int pipe_streams(sg_ctx* c, RecordStaging* rs, int i, PipeStreams* out) {
 // the host's event polling and late enqueues idled the copy engines.)
 // more(): whether another chunk is to be staged (the reader stops at a failed
 // record).
+// The pipeline of sg_write_records / sg_read_records.  Chunk k uses slot
+// k % ns and passes four steps:
+//   stage    host framing copy (staged path) and the H2D, when the slot is free;
+//   launch   the kernels, once the chunk's H2D has completed;
+//   copy_out the D2H, once the chunk's kernels have completed;
+//   finish   host framing (oldest chunk first), once the chunk's D2H has completed.
+// Each step is enqueued by the calling thread when the step before it has
+// completed on the device (hipEventQuery, polled every few microseconds), so
+// no stream ever holds a device-side wait.  That matters once two contexts run
+// at once (suruga's reader and writer, client.rs:19-24, 269-271): a copy
+// enqueued ahead of its input waits inside the DMA engine's queue and holds up
+// every later copy of the process on that engine and, when the process has more
+// streams than hardware queues (GPU_MAX_HW_QUEUES = 4), every command of the
+// streams that share its queue.  Round 5's form enqueued a chunk's whole chain
+// at once with hipStreamWaitEvent between the streams: one direction at a time
+// it is as fast (33.7 / 31.5 GiB/s registered, in the bench process), but a
+// reader and a writer at once ran at 19.9 GiB/s together, 0.61x one after the
+// other; host-gated they run at 36.4, 1.28-1.44x (profiles/r06/, r06j-r06k).
+// SG_RECORD_DEVICE_WAITS=1 gives the round-5 form (A/B).  more(): whether
+// another chunk is to be staged (the reader stops at a failed record).
+bool record_device_waits() {
+    static const bool on = [] {
+        const char* e = std::getenv("SG_RECORD_DEVICE_WAITS");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
 template <class Streams, class More, class Stage, class Launch, class CopyOut, class Finish>
 int run_pipeline(RecordStaging* rs, int ns, Streams streams, More more, Stage stage, Launch launch, CopyOut copy_out,
                  Finish finish) {
-    uint64_t staged = 0, done = 0;
+    uint64_t staged = 0, launched = 0, copied = 0, done = 0;
     auto slot = [&](uint64_t k) -> RecordStaging::Slot& { return rs->slot[k % (uint64_t)ns]; };
-    int rc;
-    for (;;) {
-        if (staged < done + (uint64_t)ns && more()) {
-            RecordStaging::Slot& s = slot(staged);
-            const PipeStreams& P = streams(s);
-            s.busy = true;  // (before the enqueues: SlotReset then drains its streams on an error)
-            if ((rc = stage(s)) != SG_OK) return rc;
-            if (P.krn != P.h2d) SG_HIP(hipStreamWaitEvent(P.krn, s.ev[1], 0));
-            if ((rc = launch(s)) != SG_OK) return rc;
-            if (P.d2h != P.krn) SG_HIP(hipStreamWaitEvent(P.d2h, s.ev[2], 0));
-            if ((rc = copy_out(s)) != SG_OK) return rc;
-            ++staged;
-            continue;
-        }
-        if (done == staged) return SG_OK;
-        RecordStaging::Slot& s = slot(done);
-        SG_HIP(hipEventSynchronize(s.ev[3]));
-        if ((rc = account(s)) != SG_OK) return rc;
-        if ((rc = finish(s)) != SG_OK) return rc;
+    auto finish_oldest = [&](RecordStaging::Slot& s) -> int {
+        int r;
+        if ((r = account(s)) != SG_OK) return r;
+        if ((r = finish(s)) != SG_OK) return r;
         s.busy = false;
         ++done;
+        return SG_OK;
+    };
+    int rc;
+    if (record_device_waits()) {  // round 5: the chain enqueued at once, ordered on the device
+        for (;;) {
+            if (staged < done + (uint64_t)ns && more()) {
+                RecordStaging::Slot& s = slot(staged);
+                const PipeStreams& P = streams(s);
+                s.busy = true;  // (before the enqueues: SlotReset then drains its streams on an error)
+                if ((rc = stage(s)) != SG_OK) return rc;
+                if (P.krn != P.h2d) SG_HIP(hipStreamWaitEvent(P.krn, s.ev[1], 0));
+                if ((rc = launch(s)) != SG_OK) return rc;
+                if (P.d2h != P.krn) SG_HIP(hipStreamWaitEvent(P.d2h, s.ev[2], 0));
+                if ((rc = copy_out(s)) != SG_OK) return rc;
+                ++staged;
+                continue;
+            }
+            if (done == staged) return SG_OK;
+            SG_HIP(hipEventSynchronize(slot(done).ev[3]));
+            if ((rc = finish_oldest(slot(done))) != SG_OK) return rc;
+        }
+    }
+    // 1: the step's event has completed, 0: not yet, < 0: error
+    auto ready = [&](RecordStaging::Slot& s, int ev) -> int {
+        const hipError_t q = hipEventQuery(s.ev[ev]);
+        if (q == hipSuccess) return 1;
+        if (q == hipErrorNotReady) return 0;
+        return hip_fail(q, "hipEventQuery");
+    };
+    for (;;) {
+        bool progress = false;
+        if (copied > done) {
+            if ((rc = ready(slot(done), 3)) < 0) return rc;
+            if (rc) {
+                if ((rc = finish_oldest(slot(done))) != SG_OK) return rc;
+                progress = true;
+            }
+        }
+        if (launched > copied) {
+            if ((rc = ready(slot(copied), 2)) < 0) return rc;
+            if (rc) {
+                if ((rc = copy_out(slot(copied))) != SG_OK) return rc;
+                ++copied;
+                progress = true;
+            }
+        }
+        if (staged > launched) {
+            if ((rc = ready(slot(launched), 1)) < 0) return rc;
+            if (rc) {
+                if ((rc = launch(slot(launched))) != SG_OK) return rc;
+                ++launched;
+                progress = true;
+            }
+        }
+        if (staged < done + (uint64_t)ns && more()) {
+            RecordStaging::Slot& s = slot(staged);
+            s.busy = true;
+            if ((rc = stage(s)) != SG_OK) return rc;
+            ++staged;
+            progress = true;
+        }
+        if (done == staged && !more()) return SG_OK;
+        if (!progress) {
+            // ~5 us between polls: polling back to back slowed the copies
+            // (20.6 instead of 33.5 GiB/s registered write, r06a), and a
+            // sleep rounds up to the kernel's timer slack (~50 us)
+            const auto t0 = std::chrono::steady_clock::now();
+            while (std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(5)) _mm_pause();
+        }
     }
 }
 

@@ -148,3 +148,34 @@ class Sampler:
                 "sources": {k: os.path.basename(v) for k, v in self.files.items()},
                 "sclk_mhz": stats("sclk_mhz", inside), "board_power_w": power, **self.static,
                 "period_s": self.period}
+
+
+def parse_cpulist(text: str) -> list[int]:
+    """'0-3,8,10-11' -> [0, 1, 2, 3, 8, 10, 11]"""
+    cpus = []
+    for part in (text or "").strip().split(","):
+        if not part:
+            continue
+        lo, _, hi = part.partition("-")
+        cpus.extend(range(int(lo), int(hi or lo) + 1))
+    return cpus
+
+
+def pin_to_gpu_node(pci_bus_id: str | None, drm: str = DRM):
+    """Restrict the calling process to the CPUs of the GPU's own NUMA node
+    (the card's `local_cpulist`, intersected with the CPUs it may use), so that
+    host buffers first touched afterwards, and the record layer's copy threads
+    created afterwards, sit next to the card's host link.  Without it a
+    host-memory measurement lands on either socket of a two-socket host and
+    its rate varies by tens of percent between runs.  Returns (cpus or None,
+    how it was chosen); changes nothing when the card or its list is missing."""
+    card, how = pick_card(pci_bus_id, drm)
+    if card is None:
+        return None, how
+    local = set(parse_cpulist(_read(os.path.join(card, "local_cpulist")) or ""))
+    allowed = set(os.sched_getaffinity(0))
+    cpus = sorted(local & allowed)
+    if not cpus:
+        return None, "no CPU of the card's node is available to this process"
+    os.sched_setaffinity(0, cpus)
+    return cpus, f"{how}, NUMA-local CPUs"

@@ -38,10 +38,21 @@ def test_bench_help():
 @pytest.mark.gpu
 def test_bench_single_gpu_small(gpu):
     p = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--records", "4096", "--steps", "2", "--warmup", "1",
-                        "--no-cpu-baseline"], capture_output=True, text=True, timeout=300, cwd=ROOT)
+                        "--no-cpu-baseline", "--record-path-bytes", str(24 << 20)], capture_output=True, text=True,
+                       timeout=300, cwd=ROOT)
     assert p.returncode == 0, p.stderr[-3000:]
     j = _last_json(p.stdout)
     assert KEYS <= set(j) and j["n_gpus"] == 1 and j["correct"] and j["value"] > 0
+    # the copy-inclusive record path: pageable and registered
+    # buffers, each one direction at a time and duplex, every byte verified and a
+    # sample of the wire against the oracle
+    rp = j["record_path"]
+    assert rp["correct"] and rp["bytes"] == 24 << 20
+    for mode in ("pageable", "registered"):
+        r = rp[mode]
+        assert r["correct"] and r["wire_sample_ok"] and r["duplex"]["correct"] and r["registered"] == (mode == "registered")
+        assert r["write_gibs"] > 0 and r["read_gibs"] > 0 and r["duplex"]["gibs"] > 0
+        assert set(r["write_split"]) == {"h2d_ms_per_gib", "kernel_ms_per_gib", "d2h_ms_per_gib", "host_ms_per_gib"}
     assert set(j["roofline"]) >= {"bound", "achieved", "peak", "unit", "frac", "traffic"}
     # the C2 sub-record (BASELINE configs[2]) under the same protocol, checked against the oracle
     c2 = j["c2"]
@@ -173,7 +184,8 @@ def test_bench_local_rank_maps_to_visible_device(gpu):
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "MASTER_PORT")}
     env["LOCAL_RANK"] = "1"
     p = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--records", "4096", "--steps", "2", "--warmup", "1",
-                        "--no-cpu-baseline"], capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
+                        "--no-cpu-baseline", "--record-path-bytes", "0"], capture_output=True, text=True, timeout=300,
+                       cwd=ROOT, env=env)
     assert p.returncode == 0, p.stderr[-3000:]
     j = _last_json(p.stdout)
     nd = torch.cuda.device_count()

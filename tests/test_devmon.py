@@ -51,3 +51,13 @@ def test_sampler_without_card_reports_none(tmp_path):
     (tmp_path / "drm").mkdir()
     m = devmon.Sampler("0000:dc:00.0", drm=str(tmp_path / "drm")).start().stop()
     assert m["sclk_mhz"] is None and m["board_power_w"] is None and m["card"] is None
+
+
+def test_parse_cpulist_and_pin_without_card(tmp_path):
+    from suruga_amd import devmon
+
+    assert devmon.parse_cpulist("0-3,8,10-11\n") == [0, 1, 2, 3, 8, 10, 11]
+    assert devmon.parse_cpulist("") == []
+    before = os.sched_getaffinity(0)
+    cpus, how = devmon.pin_to_gpu_node("0000:aa:00.0", drm=str(tmp_path))  # no card: nothing changes
+    assert cpus is None and os.sched_getaffinity(0) == before

@@ -13,7 +13,7 @@ for i in $(seq 1 "$R"); do
   for spec in "$@"; do
     name=${spec%%=*}; lib=${spec#*=}
     if [ "$lib" = "-" ]; then lib=suruga_amd/libsuruga_gpu.so; fi
-    SURUGA_ALLOW_VARIANT=${SURUGA_ALLOW_VARIANT:-1} SURUGA_GPU_LIB=$lib timeout -k 10 300 python bench.py --no-cpu-baseline --no-bitexact --steps 10 --c2-steps 0 ${BENCH_ARGS:-} > "$OUT/${name}_$i.json"
+    SURUGA_ALLOW_VARIANT=${SURUGA_ALLOW_VARIANT:-1} SURUGA_GPU_LIB=$lib timeout -k 10 300 python bench.py --no-cpu-baseline --no-bitexact --steps 10 --c2-steps 0 --record-path-bytes 0 ${BENCH_ARGS:-} > "$OUT/${name}_$i.json"
     rc=$?
     # rc 3 = ran but not correct: accepted for timing-only variants (AB_ALLOW_WRONG=1)
     if [ $rc -ne 0 ] && ! { [ $rc -eq 3 ] && [ "${AB_ALLOW_WRONG:-0}" = 1 ]; }; then echo "$name rc=$rc"; exit $rc; fi

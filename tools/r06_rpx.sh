@@ -1,9 +1,20 @@
+# round-6 record-path pipeline A/B (SG_PIPE modes x SG_RECORD_SLOTS), standalone and inside bench.py
 set -uo pipefail
-O=gpurun_out/r06b; mkdir -p $O
-for cfg in "dw0:SG_PIPE_DEVWAIT=0" "dw1:SG_PIPE_DEVWAIT=1" "dw2:SG_PIPE_DEVWAIT=2" "cs0:SG_COPY_STREAMS=0" "dw2cs0:SG_PIPE_DEVWAIT=2 SG_COPY_STREAMS=0"; do
-  name=${cfg%%:*}; envs=${cfg#*:}
-  env $envs timeout -k 10 200 python -u tools/record_path_bench.py --threads 8 --registered 1 --json-out $O/rp_$name.json > $O/rp_$name.log 2>&1 || { echo "$name failed"; tail -5 $O/rp_$name.log; exit 1; }
-  python -c "
-import json; j=json.load(open('$O/rp_$name.json'))
-for k,r in j['by_copy_threads'].items(): print('$name', k, r['write_gibs'], r['read_gibs'], 'duplex', r['duplex']['gibs'], r['duplex']['vs_slower_single'], r['write_split'])"
+O=gpurun_out/${1:-r06g}; mkdir -p $O
+CFGS=${CFGS:-"0:3 1:4 1:6 2:4 2:6 3:4 3:6"}
+for cfg in $CFGS; do
+  m=${cfg%%:*}; rest=${cfg#*:}; ns=${rest%%:*}; pu=${rest#*:}; [ "$pu" = "$rest" ] && pu=-1; pr=${PRIO:-0}; t=p${m}s${ns}u${pu}r$pr; export SG_PIPE_POLL_US=$pu SG_PIPE_PRIO=$pr
+  SG_PIPE=$m SG_RECORD_SLOTS=$ns timeout -k 10 200 python -u tools/record_path_bench.py --threads 8 --registered 0,1 --json-out $O/rp_$t.json > $O/rp_$t.log 2>&1 || { echo "$t failed"; tail -5 $O/rp_$t.log; exit 1; }
+  SG_PIPE=$m SG_RECORD_SLOTS=$ns timeout -k 10 300 python -u bench.py --steps 3 --warmup 1 --c2-steps 3 --no-cpu-baseline --no-bitexact --energy-seconds 0 > $O/bench_$t.json 2> $O/bench_$t.err || { echo "bench $t failed"; tail -5 $O/bench_$t.err; exit 1; }
+  python - $O $t <<'PY'
+import json, sys
+o, t = sys.argv[1], sys.argv[2]
+j = json.load(open(f"{o}/rp_{t}.json"))
+for k, r in j["by_copy_threads"].items():
+    print(t, "standalone", k, r["write_gibs"], r["read_gibs"], "duplex", r["duplex"]["gibs"], "vs_serial", r["duplex"]["vs_serial"], r["correct"] and r["duplex"]["correct"])
+b = json.loads(open(f"{o}/bench_{t}.json").read().strip().splitlines()[-1])["record_path"]
+for k in ("pageable", "registered"):
+    r = b[k]
+    print(t, "in-bench  ", k, r["write_gibs"], r["read_gibs"], "duplex", r["duplex"]["gibs"], "vs_serial", r["duplex"]["vs_serial"], r["correct"] and r["duplex"]["correct"] and r["wire_sample_ok"])
+PY
 done
