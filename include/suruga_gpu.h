@@ -197,9 +197,11 @@ int sg_open_batch(const sg_batch* b);
 
 /* ---- batched record layer over host memory ------------------------------
  * The throughput form of TlsWriter / TlsReader (tls.rs:68-380): many records
- * per call, pipelined host<->device copies inside the library (three chunks
- * of 256 records in flight: one coming in, one in the kernels, one going out;
- * pinned staging for unregistered buffers), wire format exactly as the
+ * per call, pipelined host<->device copies inside the library (four chunks
+ * of 256 records in flight: coming in, in the kernels, going out; each step
+ * enqueued by the calling thread once the step before it has completed, so
+ * that a reader and a writer on two contexts never queue behind each other's
+ * unfinished work; pinned staging for unregistered buffers), wire format exactly as the
  * reference writes and parses it:
  *   header = content_type || major || minor || be16(fragment length)
  *   (tls.rs:126-130, 218-236) followed by the fragment (ct || tag).        */
