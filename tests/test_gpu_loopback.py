@@ -4,8 +4,9 @@ TlsReader data path of tls.rs:126-147 and :238-281 with the handshake
 bypassed as in src/test.rs:29-39).  Every wire byte the writer sent is
 compared with the oracle's TLS sealing of the same records (header, ct, tag:
 chacha20_poly1305.rs:48-59, tls.rs:103-112), and every byte the reader
-delivered with the stream that went in.  Also the copy-inclusive record path
-per direction (tools/record_path_bench.py) at a reduced size.
+delivered with the stream that went in, at 64 MiB and at C4's full 1 GiB.
+Also the copy-inclusive record path per direction and duplex
+(tools/record_path_bench.py) at a reduced size.
 """
 from __future__ import annotations
 
@@ -25,10 +26,13 @@ KEY_C2S = bytes(range(32))
 REC = 1 << 14
 
 
-def test_loopback_64mib_wire_equals_oracle(gpu, oracle):
+@pytest.mark.parametrize("total", [64 << 20, 1 << 30], ids=["64MiB", "1GiB"])
+def test_loopback_wire_equals_oracle(gpu, oracle, total):
+    """64 MiB, and C4's full 1 GiB stream (BASELINE.json configs[4]): every
+    wire record against the oracle, every delivered byte against the input."""
     import tls_loopback as TL
 
-    total, wchunk = 64 << 20, 16 << 20
+    wchunk = 16 << 20
     res = TL.run(total, wchunk, 0, capture=True)
     assert res["correct"], {k: v for k, v in res.items() if k != "wire"}
     assert res["reader"]["bytes"] == total and res["reader"]["mismatched_bytes"] == 0
@@ -48,26 +52,31 @@ def test_loopback_64mib_wire_equals_oracle(gpu, oracle):
 def test_record_path_both_directions_bit_exact(gpu):
     import record_path_bench as RP
 
-    r = RP.one(32 << 20, 8 << 20, 0)
-    assert r["correct"], r
-    assert r["records"] == (32 << 20) // REC
+    for registered in (False, True):
+        r = RP.one(32 << 20, 8 << 20, 0, registered)
+        assert r["correct"], r
+        assert r["records"] == (32 << 20) // REC
+        # a writer and a reader on two contexts at once: both outputs bit-exact
+        assert r["duplex"]["correct"] and not r["duplex"]["errors"], r["duplex"]
 
 
+@pytest.mark.parametrize("total", [64 << 20, 1 << 30], ids=["64MiB", "1GiB"])
 @pytest.mark.parametrize("registered", [False, True])
-def test_cpp_loopback_every_byte(gpu, registered):
+def test_cpp_loopback_every_byte(gpu, registered, total):
     """tools/loopback_cpp (C4 in C++ over include/suruga, no Python on the data
-    path): 64 MiB over a loopback socket, staged and zero-copy (registered
-    buffers); the harness compares every delivered byte with the stream."""
+    path): 64 MiB and C4's full 1 GiB over a loopback socket, staged and
+    zero-copy (registered buffers); the harness compares every delivered byte
+    with the stream."""
     import json
     import subprocess
 
     from suruga_amd import _build
 
     exe = _build.build_loopback_cpp()
-    args = [str(exe), "--bytes", str(64 << 20), "--chunk", str(8 << 20), "--block", str(8 << 20)]
+    args = [str(exe), "--bytes", str(total), "--chunk", str(8 << 20), "--block", str(8 << 20)]
     p = subprocess.run(args + (["--registered"] if registered else []), capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stdout + p.stderr
     j = json.loads(p.stdout.strip().splitlines()[-1])
     assert j["correct"] and j["registered"] is registered
-    assert j["reader"]["bytes"] == 64 << 20 and j["reader"]["mismatched_bytes"] == 0
-    assert j["writer"]["records"] == (64 << 20) // REC == j["reader"]["records"]
+    assert j["reader"]["bytes"] == total and j["reader"]["mismatched_bytes"] == 0
+    assert j["writer"]["records"] == total // REC == j["reader"]["records"]
