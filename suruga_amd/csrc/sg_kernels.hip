@@ -733,15 +733,27 @@ __global__ __launch_bounds__(256) void sg_frame_kernel(const uint8_t* __restrict
 }
 
 // dst + r * dst_stride <- the frag bytes of wire record r (src + r * pitch + 5),
-// count records of one fragment length (src readable 4 bytes past the image).
+// count records of one fragment length.  The image is count * pitch bytes; a
+// word whose aligned loads would reach past it is read byte by byte, so that
+// no load leaves the image (src may be the caller's registered host buffer,
+// read over the host link, whose next page need not be mapped).
 __global__ __launch_bounds__(256) void sg_unframe_kernel(const uint8_t* __restrict__ src, uint32_t pitch,
                                                          uint8_t* __restrict__ dst, uint32_t dst_stride,
                                                          uint32_t count, uint32_t frag) {
     const uint32_t wpr = (frag + 3u) >> 2;  // destination words per record
     const uint32_t total = wpr * count;
+    const uint64_t image = (uint64_t)count * pitch;
     for (uint32_t g = blockIdx.x * 256u + threadIdx.x; g < total; g += gridDim.x * 256u) {
         const uint32_t r = g / wpr, w = g - r * wpr;
-        const uint32_t v = ld_u32_unaligned(src + (uint64_t)r * pitch + SG_HEADER_LEN + 4u * w);
+        const uint64_t off = (uint64_t)r * pitch + SG_HEADER_LEN + 4u * w;
+        const uint64_t a0 = ((uintptr_t)src + off) & 3u;  // the aligned loads cover [off - a0, off - a0 + 8)
+        uint32_t v;
+        if (off - a0 + 8u <= image && off >= a0) {
+            v = ld_u32_unaligned(src + off);
+        } else {
+            v = 0u;
+            for (uint32_t k = 0; k < 4u && off + k < image; ++k) v |= (uint32_t)src[off + k] << (8u * k);
+        }
         uint8_t* d = dst + (uint64_t)r * dst_stride + 4u * w;
         if (4u * w + 4u <= frag) {
             *reinterpret_cast<uint32_t*>(d) = v;

@@ -151,6 +151,10 @@ struct RecordStaging {
         uint8_t *d_in = nullptr, *d_out = nullptr, *d_meta = nullptr, *d_status = nullptr;
         uint8_t* d_wire = nullptr;  // the chunk's wire image (zero-copy path)
         uint32_t* d_len = nullptr;
+        // device addresses of the pinned blocks (the direct pipeline's kernels
+        // read and write them over the host link)
+        uint8_t *dh_in = nullptr, *dh_out = nullptr, *dh_meta = nullptr, *dh_status = nullptr;
+        uint32_t* dh_len = nullptr;
         void* d_ws = nullptr;
         hipStream_t st = nullptr;  // SG_COPY_STREAMS=0 only: the slot's copies and kernels
         hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};  // start, after H2D, after kernels, after D2H
@@ -158,8 +162,10 @@ struct RecordStaging {
         uint64_t first = 0;      // index of its first record in the call
         bool zc = false;         // the chunk goes the zero-copy way
         bool busy = false;
+        hipStream_t kst = nullptr;  // direct pipeline: the stream of the chunk's kernels
     } slot[kMaxSlots];
-    hipStream_t krn = nullptr;  // the context's kernel stream (copy-stream mode 1)
+    hipStream_t krn = nullptr;  // the copy-engine pipeline's kernel stream (copy-stream mode 1)
+    hipStream_t kst = nullptr;  // the direct pipeline's stream
 };
 
 // Pipeline depth (SG_RECORD_SLOTS, 2..8).  Four slots (default since round 6)
@@ -199,6 +205,17 @@ int copy_streams_mode() {
     }();
     return m;
 }
+// The direct pipeline for staged calls (round 6, default; run_direct): the
+// record kernels read the pinned staging and write their output into it over
+// the host link themselves.  SG_RECORD_SDMA=1: the copy-engine pipeline
+// (run_pipeline) for staged calls too (A/B).
+bool record_direct() {
+    static const bool on = [] {
+        const char* e = std::getenv("SG_RECORD_SDMA");
+        return !(e && e[0] == '1');
+    }();
+    return on;
+}
 std::mutex g_cs_mu;
 std::vector<std::pair<int, std::pair<hipStream_t, hipStream_t>>> g_copy_streams;  // device -> (h2d, d2h)
 hipError_t process_copy_streams(int dev, hipStream_t* h2d, hipStream_t* d2h) {
@@ -219,9 +236,10 @@ hipError_t process_copy_streams(int dev, hipStream_t* h2d, hipStream_t* d2h) {
 void record_staging_free(RecordStaging* rs) {
     if (!rs) return;
 
-    if (rs->krn) {
-        (void)hipStreamSynchronize(rs->krn);
-        (void)hipStreamDestroy(rs->krn);
+    for (hipStream_t t : {rs->krn, rs->kst}) {
+        if (!t) continue;
+        (void)hipStreamSynchronize(t);
+        (void)hipStreamDestroy(t);
     }
     for (auto& s : rs->slot) {
         if (s.st) (void)hipStreamSynchronize(s.st);
@@ -259,16 +277,15 @@ int staging(sg_ctx* c, RecordStaging** out) {
         // GiB/s registered with the kernels on a context stream created before
         // the copy streams, r06l, against 35.1 in a process whose other
         // streams happened to separate them)
-        if (copy_streams_mode() != 0) {
-            hipStream_t h = nullptr, d = nullptr;
-            SG_HIP(process_copy_streams(c->device, &h, &d));
-            SG_HIP(hipStreamCreateWithFlags(&rs->krn, hipStreamNonBlocking));
-        }
+        // (the streams are created by pipe_streams on a call's first use of them)
         for (int i = 0; i < record_slots(); ++i) {  // (h_in / h_out: host_staging, on first use)
             auto& s = rs->slot[i];
-            SG_HIP(hipHostMalloc((void**)&s.h_meta, (size_t)kChunk * kMetaBytes, hipHostMallocDefault));
-            SG_HIP(hipHostMalloc((void**)&s.h_status, kChunk, hipHostMallocDefault));
-            SG_HIP(hipHostMalloc((void**)&s.h_len, kChunk * 4u, hipHostMallocDefault));
+            SG_HIP(hipHostMalloc((void**)&s.h_meta, (size_t)kChunk * kMetaBytes, hipHostMallocMapped));
+            SG_HIP(hipHostMalloc((void**)&s.h_status, kChunk, hipHostMallocMapped));
+            SG_HIP(hipHostMalloc((void**)&s.h_len, kChunk * 4u, hipHostMallocMapped));
+            SG_HIP(hipHostGetDevicePointer((void**)&s.dh_meta, s.h_meta, 0));
+            SG_HIP(hipHostGetDevicePointer((void**)&s.dh_status, s.h_status, 0));
+            SG_HIP(hipHostGetDevicePointer((void**)&s.dh_len, s.h_len, 0));
             SG_HIP(hipMalloc((void**)&s.d_in, bytes));
             SG_HIP(hipMalloc((void**)&s.d_out, bytes));
             SG_HIP(hipMalloc((void**)&s.d_wire, bytes + 64));
@@ -276,7 +293,6 @@ int staging(sg_ctx* c, RecordStaging** out) {
             SG_HIP(hipMalloc((void**)&s.d_status, kChunk));
             SG_HIP(hipMalloc((void**)&s.d_len, kChunk * 4u));
             SG_HIP(hipMalloc(&s.d_ws, sg_workspace_size(kChunk)));
-            if (copy_streams_mode() == 0) SG_HIP(hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking));
             for (auto& e : s.ev) SG_HIP(hipEventCreate(&e));
         }
     }
@@ -288,8 +304,14 @@ int staging(sg_ctx* c, RecordStaging** out) {
 // them, so a context that only moves registered buffers pins no staging).
 int host_staging(RecordStaging::Slot& s) {
     const size_t bytes = (size_t)kChunk * kSlot;
-    if (!s.h_in) SG_HIP(hipHostMalloc((void**)&s.h_in, bytes, hipHostMallocDefault));
-    if (!s.h_out) SG_HIP(hipHostMalloc((void**)&s.h_out, bytes, hipHostMallocDefault));
+    if (!s.h_in) {
+        SG_HIP(hipHostMalloc((void**)&s.h_in, bytes, hipHostMallocMapped));
+        SG_HIP(hipHostGetDevicePointer((void**)&s.dh_in, s.h_in, 0));
+    }
+    if (!s.h_out) {
+        SG_HIP(hipHostMalloc((void**)&s.h_out, bytes, hipHostMallocMapped));
+        SG_HIP(hipHostGetDevicePointer((void**)&s.dh_out, s.h_out, 0));
+    }
     return SG_OK;
 }
 
@@ -331,31 +353,26 @@ struct SlotReset {
 };
 
 // the streams of slot i for this call (mode: copy_streams_mode)
-int pipe_streams(sg_ctx* c, RecordStaging* rs, int i, PipeStreams* out) {
+int pipe_streams(sg_ctx* c, RecordStaging* rs, int i, bool direct, PipeStreams* out) {
+    if (direct) {
+        if (!rs->kst) SG_HIP(hipStreamCreateWithFlags(&rs->kst, hipStreamNonBlocking));
+        *out = {rs->kst, rs->kst, rs->kst};
+        return SG_OK;
+    }
     if (copy_streams_mode() == 0) {
+        if (!rs->slot[i].st) SG_HIP(hipStreamCreateWithFlags(&rs->slot[i].st, hipStreamNonBlocking));
         *out = {rs->slot[i].st, rs->slot[i].st, rs->slot[i].st};
         return SG_OK;
     }
+    // the process's copy streams first, then the context's kernel stream: HIP
+    // hands a process's streams its hardware queues round-robin
     hipStream_t h = nullptr, d = nullptr;
     SG_HIP(process_copy_streams(c->device, &h, &d));
+    if (!rs->krn) SG_HIP(hipStreamCreateWithFlags(&rs->krn, hipStreamNonBlocking));
     *out = {h, rs->krn, d};
     return SG_OK;
 }
 
-// The pipeline of sg_write_records / sg_read_records.  Chunk k uses slot
-// k % ns and passes four steps: stage (host framing copy on the staged path,
-// the H2D), launch (the kernels, on the device after the H2D), copy_out (the
-// D2H, on the device after the kernels) and finish (host framing, oldest chunk
-// first, once the D2H has completed).  The first three are enqueued together,
-// up to ns chunks ahead of the oldest unfinished one, with the cross-stream
-// order kept on the device (hipStreamWaitEvent), so the host only ever waits
-// for the oldest chunk's D2H.  (Round 6 measured a host-driven form, each step
-// enqueued only once the previous one had completed on the device, so that no
-// stream ever holds a device-side wait: 20.6 / 19.6 GiB/s registered write /
-// read against 33.4 / 30.7 for this form on the same box, profiles/r06c --
-// the host's event polling and late enqueues idled the copy engines.)
-// more(): whether another chunk is to be staged (the reader stops at a failed
-// record).
 // The pipeline of sg_write_records / sg_read_records.  Chunk k uses slot
 // k % ns and passes four steps:
 //   stage    host framing copy (staged path) and the H2D, when the slot is free;
@@ -373,9 +390,54 @@ int pipe_streams(sg_ctx* c, RecordStaging* rs, int i, PipeStreams* out) {
 // at once with hipStreamWaitEvent between the streams: one direction at a time
 // it is as fast (33.7 / 31.5 GiB/s registered, in the bench process), but a
 // reader and a writer at once ran at 19.9 GiB/s together, 0.61x one after the
-// other; host-gated they run at 36.4, 1.28-1.44x (profiles/r06/, r06j-r06k).
+// other; host-gated they run at 36.4, 1.1-1.4x (profiles/r06/record_path_ab/).
+// Polling back to back slowed the copies (20.6 instead of 33.5 GiB/s
+// registered write, profiles/r06/record_path_hostdriven.json), so the host
+// waits ~5 us between polls.
 // SG_RECORD_DEVICE_WAITS=1 gives the round-5 form (A/B).  more(): whether
 // another chunk is to be staged (the reader stops at a failed record).
+// The direct pipeline (round 6; the staged path, record_direct): the record
+// kernels read the pinned staging and write their output into it over the
+// host link themselves, so no copy engine is involved and a chunk's work is
+// the kernels of one stream.  The host keeps up to ns chunks in flight, fills
+// the next slot's staging while the GPU works, and waits only for the oldest
+// chunk before reusing its slot.  On this host link kernels move data faster
+// than the copy engines (tools/hostbw_probe.hip, profiles/r06/hostbw_r06t.txt:
+// kernel stores to host memory 54.8 GB/s, loads 57.3 GB/s, against 30.2 / 40.6
+// GB/s for SDMA D2H / H2D, and 28.6 GB/s each with a copy in each direction at
+// once).  Zero-copy calls keep the copy-engine pipeline: there the seal kernel
+// reading the caller's buffer and the frame kernel writing the wire reached
+// 20-23 GiB/s against 34.6 / 24.1 GiB/s write / read for SDMA copies
+// (profiles/r06/record_path_ab/, r06u-r06v).
+template <class More, class Stage, class Launch, class Finish>
+int run_direct(RecordStaging* rs, int ns, More more, Stage stage, Launch launch, Finish finish) {
+    uint64_t staged = 0, done = 0;
+    auto slot = [&](uint64_t k) -> RecordStaging::Slot& { return rs->slot[k % (uint64_t)ns]; };
+    int rc;
+    for (;;) {
+        if (staged < done + (uint64_t)ns && more()) {
+            RecordStaging::Slot& s = slot(staged);
+            s.busy = true;  // (before the enqueues: SlotReset then drains the streams on an error)
+            s.kst = rs->kst;
+            if ((rc = stage(s)) != SG_OK) return rc;
+            SG_HIP(hipEventRecord(s.ev[0], s.kst));
+            if ((rc = launch(s)) != SG_OK) return rc;
+            SG_HIP(hipEventRecord(s.ev[3], s.kst));
+            ++staged;
+            continue;
+        }
+        if (done == staged) return SG_OK;
+        RecordStaging::Slot& s = slot(done);
+        SG_HIP(hipEventSynchronize(s.ev[3]));
+        float ms = 0;
+        SG_HIP(hipEventElapsedTime(&ms, s.ev[0], s.ev[3]));
+        t_kernel += ms;  // (the chunks on the two streams overlap: device time, not wall time)
+        if ((rc = finish(s)) != SG_OK) return rc;
+        s.busy = false;
+        ++done;
+    }
+}
+
 bool record_device_waits() {
     static const bool on = [] {
         const char* e = std::getenv("SG_RECORD_DEVICE_WAITS");
@@ -482,17 +544,19 @@ inline void put_be64(uint8_t* p, uint64_t v) {
 // chunk's wire image (headers and fragments) in HBM and copies it out with one
 // contiguous D2H; sg_read_records copies the chunk's wire image in, takes it
 // apart in HBM and copies the plaintext out contiguously.
+struct RegRange {
+    uintptr_t lo, hi;  // [lo, hi)
+};
 std::mutex g_reg_mu;
-std::vector<std::pair<uintptr_t, uintptr_t>> g_reg;  // [lo, hi)
+std::vector<RegRange> g_reg;
 bool registered(const void* p, size_t n) {
     if (!p || !n) return false;
     const uintptr_t lo = (uintptr_t)p, hi = lo + n;
     std::lock_guard<std::mutex> lk(g_reg_mu);
     for (const auto& r : g_reg)
-        if (lo >= r.first && hi <= r.second) return true;
+        if (lo >= r.lo && hi <= r.hi) return true;
     return false;
 }
-
 // SG_ZERO_COPY=0 in the environment turns the registered-buffer path off (A/B)
 bool zero_copy_enabled() {
     static const bool on = [] {
@@ -519,7 +583,7 @@ int sg_host_register(void* p, size_t len) {
     const hipError_t e = hipHostRegister(p, len, hipHostRegisterPortable);
     if (e != hipSuccess) return sg::hip_fail(e, "hipHostRegister");
     std::lock_guard<std::mutex> lk(sg::g_reg_mu);
-    sg::g_reg.emplace_back((uintptr_t)p, (uintptr_t)p + len);
+    sg::g_reg.push_back({(uintptr_t)p, (uintptr_t)p + len});
     return SG_OK;
 }
 
@@ -527,7 +591,7 @@ int sg_host_unregister(void* p) {
     {
         std::lock_guard<std::mutex> lk(sg::g_reg_mu);
         auto it = std::find_if(sg::g_reg.begin(), sg::g_reg.end(),
-                               [&](const std::pair<uintptr_t, uintptr_t>& r) { return r.first == (uintptr_t)p; });
+                               [&](const sg::RegRange& r) { return r.lo == (uintptr_t)p; });
         if (it == sg::g_reg.end()) return fail(SG_E_ARG, "range was not registered with sg_host_register%s");
         sg::g_reg.erase(it);
     }
@@ -558,20 +622,23 @@ int64_t sg_write_records(sg_ctx* c, uint64_t seq0, uint8_t content_type, uint8_t
     RecordStaging* rs = nullptr;
     int rc = staging(c, &rs);
     if (rc != SG_OK) return rc;
-    SlotReset slot_reset(rs);
-    const int ns = record_slots();
-    for (int i = 0; i < ns; ++i)
-        if ((rc = pipe_streams(c, rs, i, &slot_reset.ps[i])) != SG_OK) return rc;
-    auto streams = [&](const RecordStaging::Slot& s) -> const PipeStreams& { return slot_reset.ps[&s - rs->slot]; };
     size_t wpos = 0;
     // every record but the last is full, so record r starts at r * kWireRec
     constexpr size_t kWireRec = SG_HEADER_LEN + SG_RECORD_MAX_LEN + SG_MAC_LEN;
     const size_t wire_need = (size_t)(nrec - 1) * kWireRec + SG_HEADER_LEN +
                              (size_t)(len - (nrec - 1) * SG_RECORD_MAX_LEN) + SG_MAC_LEN;
     // registered caller buffers: DMA straight between them and the device
+    // (the copy-engine pipeline); otherwise the pinned staging, which the
+    // kernels read and write over the host link (the direct pipeline)
     const bool zc = zero_copy_enabled() && registered(data, len) && registered(wire, wire_need);
+    const bool direct = record_direct() && !zc;
     auto rec_len = [&](uint64_t r) { return (uint32_t)std::min<uint64_t>(SG_RECORD_MAX_LEN, len - r * SG_RECORD_MAX_LEN); };
     uint64_t next = 0;  // first record of the next chunk to stage
+    SlotReset slot_reset(rs);
+    const int ns = record_slots();
+    for (int i = 0; i < ns; ++i)
+        if ((rc = pipe_streams(c, rs, i, direct, &slot_reset.ps[i])) != SG_OK) return rc;
+    auto streams = [&](const RecordStaging::Slot& s) -> const PipeStreams& { return slot_reset.ps[&s - rs->slot]; };
 
     // host framing copy in, H2D (tls.rs:137-147: 2^14-byte fragments)
     auto stage = [&](RecordStaging::Slot& s) -> int {
@@ -579,7 +646,8 @@ int64_t sg_write_records(sg_ctx* c, uint64_t seq0, uint8_t content_type, uint8_t
         const double t0 = now_ms();
         // zero-copy: the chunk's plaintext is contiguous in the caller's buffer
         // (in_stride 2^14); staged: each record in its 16-byte aligned slot
-        if (zc) {
+        s.zc = zc;
+        if (s.zc) {
             for (uint32_t i = 0; i < k; ++i) s.h_len[i] = rec_len(next + i);
         } else {
             int r;
@@ -592,22 +660,22 @@ int64_t sg_write_records(sg_ctx* c, uint64_t seq0, uint8_t content_type, uint8_t
             });
         }
         t_host += now_ms() - t0;
+        s.nrec = k;
+        s.first = next;
+        next += k;
+        if (direct) return SG_OK;  // (the kernels read the input themselves)
         bool same = true;  // every record of the chunk has the same length
         for (uint32_t i = 1; i < k; ++i) same = same && s.h_len[i] == s.h_len[0];
         const hipStream_t hs = streams(s).h2d;
         SG_HIP(hipEventRecord(s.ev[0], hs));
-        if (zc) {
+        if (s.zc) {
             const size_t bytes = (size_t)(k - 1) * SG_RECORD_MAX_LEN + s.h_len[k - 1];
-            SG_HIP(hipMemcpyAsync(s.d_in, data + next * SG_RECORD_MAX_LEN, bytes, hipMemcpyHostToDevice, hs));
+            SG_HIP(hipMemcpyAsync(s.d_in, data + s.first * SG_RECORD_MAX_LEN, bytes, hipMemcpyHostToDevice, hs));
         } else {
             SG_HIP(hipMemcpyAsync(s.d_in, s.h_in, (size_t)k * kSlot, hipMemcpyHostToDevice, hs));
         }
         if (!same) SG_HIP(hipMemcpyAsync(s.d_len, s.h_len, k * 4u, hipMemcpyHostToDevice, hs));
         SG_HIP(hipEventRecord(s.ev[1], hs));
-        s.nrec = k;
-        s.first = next;
-        s.zc = zc;
-        next += k;
         return SG_OK;
     };
     // seal (and, zero-copy, the chunk's wire image: headers and fragments,
@@ -617,7 +685,7 @@ int64_t sg_write_records(sg_ctx* c, uint64_t seq0, uint8_t content_type, uint8_t
         const uint32_t k = s.nrec;
         bool same = true;
         for (uint32_t i = 1; i < k; ++i) same = same && s.h_len[i] == s.h_len[0];
-        const hipStream_t ks = streams(s).krn;
+        const hipStream_t ks = direct ? s.kst : streams(s).krn;
         sg_batch b;
         std::memset(&b, 0, sizeof b);
         b.count = k;
@@ -628,12 +696,13 @@ int64_t sg_write_records(sg_ctx* c, uint64_t seq0, uint8_t content_type, uint8_t
         b.content_type = content_type;
         b.ver_major = ver_major;
         b.ver_minor = ver_minor;
-        b.in = s.d_in;
+        // direct: straight from and into the pinned staging
+        b.in = direct ? s.dh_in : s.d_in;
         b.in_stride = s.zc ? SG_RECORD_MAX_LEN : kSlot;
-        b.out = s.d_out;
+        b.out = direct ? s.dh_out : s.d_out;
         b.out_stride = kSlot;
         // a uniform chunk is a direct launch; a ragged one (the tail) is bucketed
-        b.len = same ? nullptr : s.d_len;
+        b.len = same ? nullptr : (direct ? s.dh_len : s.d_len);
         b.uniform_len = same ? s.h_len[0] : 0u;
         b.max_len = SG_RECORD_MAX_LEN;
         b.stream = ks;
@@ -681,7 +750,9 @@ int64_t sg_write_records(sg_ctx* c, uint64_t seq0, uint8_t content_type, uint8_t
         t_host += now_ms() - t0;
         return SG_OK;
     };
-    if ((rc = run_pipeline(rs, ns, streams, [&] { return next < nrec; }, stage, launch, copy_out, finish)) != SG_OK) return rc;
+    if (direct) rc = run_direct(rs, ns, [&] { return next < nrec; }, stage, launch, finish);
+    else rc = run_pipeline(rs, ns, streams, [&] { return next < nrec; }, stage, launch, copy_out, finish);
+    if (rc != SG_OK) return rc;
     *wire_len = wpos;
     return (int64_t)nrec;
 }
@@ -720,6 +791,7 @@ int sg_read_records(sg_ctx* c, uint64_t seq0, const uint8_t* wire, size_t wire_l
     // the plaintext leaves by DMA into `out` at its final offset (prefix sum of
     // the plaintext lengths, as if every record opens)
     const bool zc = zero_copy_enabled() && registered(wire, wire_len) && registered(out, need);
+    const bool direct = record_direct() && !zc;
     std::vector<uint64_t> pre;  // zc: plaintext offset of every record
     if (zc) {
         pre.resize(nrec + 1);
@@ -744,7 +816,7 @@ int sg_read_records(sg_ctx* c, uint64_t seq0, const uint8_t* wire, size_t wire_l
     SlotReset slot_reset(rs);
     const int ns = record_slots();
     for (int i = 0; i < ns; ++i)
-        if ((rc = pipe_streams(c, rs, i, &slot_reset.ps[i])) != SG_OK) return rc;
+        if ((rc = pipe_streams(c, rs, i, direct, &slot_reset.ps[i])) != SG_OK) return rc;
     auto streams = [&](const RecordStaging::Slot& s) -> const PipeStreams& { return slot_reset.ps[&s - rs->slot]; };
 
     std::vector<uint64_t> dst_off(kChunk);
@@ -834,6 +906,12 @@ int sg_read_records(sg_ctx* c, uint64_t seq0, const uint8_t* wire, size_t wire_l
             }
         }
         t_host += now_ms() - t0;
+        if (direct) {  // (the kernels read the staging themselves)
+            s.nrec = k;
+            s.first = next;
+            next += k;
+            return SG_OK;
+        }
         const hipStream_t hs = streams(s).h2d;
         SG_HIP(hipEventRecord(s.ev[0], hs));
         if (s.zc) {  // the chunk's wire image in one contiguous copy, taken apart in HBM
@@ -862,7 +940,7 @@ int sg_read_records(sg_ctx* c, uint64_t seq0, const uint8_t* wire, size_t wire_l
             same = same && R.flen == R0.flen;
             tls = tls && R.type == R0.type && R.major == R0.major && R.minor == R0.minor;
         }
-        const hipStream_t ks = streams(s).krn;
+        const hipStream_t ks = direct ? s.kst : streams(s).krn;
         if (s.zc) SG_HIP(launch_unframe(s.d_wire, SG_HEADER_LEN + R0.flen, s.d_in, kSlot, k, R0.flen, ks));
         sg_batch b;
         std::memset(&b, 0, sizeof b);
@@ -876,20 +954,22 @@ int sg_read_records(sg_ctx* c, uint64_t seq0, const uint8_t* wire, size_t wire_l
             b.ver_major = R0.major;
             b.ver_minor = R0.minor;
         } else {
-            b.nonces = s.d_meta;
-            b.ads = s.d_meta + 8u * kChunk;
+            uint8_t* meta = direct ? s.dh_meta : s.d_meta;
+            b.nonces = meta;
+            b.ads = meta + 8u * kChunk;
             b.ad_len = 13;
             b.ad_stride = 13;
         }
-        b.in = s.d_in;
+        // direct: straight from and into the pinned staging
+        b.in = direct ? s.dh_in : s.d_in;
         b.in_stride = kSlot;
-        b.out = s.d_out;
+        b.out = direct ? s.dh_out : s.d_out;
         // zero-copy: plaintext back to back, as it lands in `out`
         b.out_stride = s.zc ? (size_t)(R0.flen - SG_MAC_LEN) : kSlot;
-        b.len = same ? nullptr : s.d_len;
+        b.len = same ? nullptr : (direct ? s.dh_len : s.d_len);
         b.uniform_len = same ? R0.flen : 0u;
         b.max_len = SG_ENC_RECORD_MAX_LEN;
-        b.status = s.d_status;
+        b.status = direct ? s.dh_status : s.d_status;
         b.stream = ks;
         b.workspace = s.d_ws;
         b.workspace_size = sg_workspace_size(kChunk);
@@ -916,9 +996,10 @@ int sg_read_records(sg_ctx* c, uint64_t seq0, const uint8_t* wire, size_t wire_l
         SG_HIP(hipEventRecord(s.ev[3], ds));
         return SG_OK;
     };
-    if ((rc = run_pipeline(rs, ns, streams, [&] { return next < nrec && error == SG_OK; }, stage, launch, copy_out, collect)) !=
-        SG_OK)
-        return rc;
+    auto more = [&] { return next < nrec && error == SG_OK; };
+    if (direct) rc = run_direct(rs, ns, more, stage, launch, collect);
+    else rc = run_pipeline(rs, ns, streams, more, stage, launch, copy_out, collect);
+    if (rc != SG_OK) return rc;
     scrub.armed = false;  // collect() has cleared whatever it did not deliver
     res->records = good;
     res->consumed = consumed;
