@@ -200,6 +200,9 @@ hipError_t launch_frame(const uint8_t* src, uint32_t src_stride, uint8_t* dst, u
                         uint32_t frag, uint32_t last_frag, uint32_t hdr, hipStream_t s);
 hipError_t launch_unframe(const uint8_t* src, uint32_t pitch, uint8_t* dst, uint32_t dst_stride, uint32_t count,
                           uint32_t frag, hipStream_t s);
+// dst[0, n) <- src[0, n) by a kernel (dst: the caller's registered host memory,
+// written over the host link; src 4-byte aligned)
+hipError_t launch_copy_out(const uint8_t* src, uint8_t* dst, uint64_t n, hipStream_t s);
 hipError_t launch_fill(uint8_t* buf, uint64_t stride, uint32_t len, uint32_t count, uint64_t seed,
                        uint64_t j0, hipStream_t s);
 hipError_t launch_compare(const uint8_t* a, uint64_t sa, const uint8_t* b, uint64_t sb, uint32_t len,

@@ -763,6 +763,31 @@ __global__ __launch_bounds__(256) void sg_unframe_kernel(const uint8_t* __restri
     }
 }
 
+// dst[0, n) <- src[0, n): the zero-copy read's plaintext from HBM into the
+// caller's registered `out` over the host link (sg_record.cpp).  src is 4-byte
+// aligned; dst may not be.  Every thread writes one 4-byte aligned word of dst
+// (a funnel shift of two source words: the lanes' stores cover whole 256-byte
+// segments) and the partial words at either end byte by byte, so that no store
+// leaves [dst, dst + n), and no load leaves [src, src + n + 3] rounded to words.
+__global__ __launch_bounds__(256) void sg_copy_out_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                         uint64_t n) {
+    const uint32_t a = (uint32_t)((4u - ((uintptr_t)dst & 3u)) & 3u);  // bytes before dst's first aligned word
+    const uint64_t nw = n > a ? (n - a) >> 2 : 0;                       // whole aligned words of dst
+    const uint64_t tid = blockIdx.x * 256ull + threadIdx.x, nth = (uint64_t)gridDim.x * 256ull;
+    if (tid < a && tid < n) dst[tid] = src[tid];
+    const uint32_t* s32 = reinterpret_cast<const uint32_t*>(src);
+    uint32_t* d32 = reinterpret_cast<uint32_t*>(dst + a);
+    for (uint64_t w = tid; w < nw; w += nth) {
+        const uint64_t b = a + 4u * w;  // source byte of the word's first byte
+        const uint64_t q = b >> 2;
+        const uint32_t lo = s32[q];
+        const uint32_t hi = (b & 3u) ? s32[q + 1] : 0u;
+        d32[w] = __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(b & 3u));
+    }
+    const uint64_t t0 = a + 4u * nw;  // the byte tail
+    if (tid < 4u && t0 + tid < n) dst[t0 + tid] = src[t0 + tid];
+}
+
 // Failed opens release no plaintext (chacha20_poly1305.rs:80-93 decrypts
 // unconditionally but returns only Err on a tag mismatch): every record whose
 // status is 1 (wrong mac) gets its output range zeroed after the open
@@ -1147,6 +1172,15 @@ hipError_t launch_frame(const uint8_t* src, uint32_t src_stride, uint8_t* dst, u
     grid = grid < 4096u ? grid : 4096u;
     hipLaunchKernelGGL(sg_frame_kernel, dim3(grid), dim3(256), 0, s, src, src_stride, dst, pitch, rdiv, count, frag,
                        last_frag, hdr);
+    return hipGetLastError();
+}
+
+hipError_t launch_copy_out(const uint8_t* src, uint8_t* dst, uint64_t n, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    if ((uintptr_t)src & 3u) return hipErrorInvalidValue;
+    uint64_t grid = (n / 4u + 255u) / 256u;
+    grid = grid < 4096u ? (grid ? grid : 1u) : 4096u;
+    hipLaunchKernelGGL(sg_copy_out_kernel, dim3((uint32_t)grid), dim3(256), 0, s, src, dst, n);
     return hipGetLastError();
 }
 

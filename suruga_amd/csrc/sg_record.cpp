@@ -148,11 +148,11 @@ struct RecordStaging {
     struct Slot {
         uint8_t *h_in = nullptr, *h_out = nullptr, *h_meta = nullptr, *h_status = nullptr;
         uint32_t* h_len = nullptr;
-        uint8_t *d_in = nullptr, *d_out = nullptr, *d_meta = nullptr, *d_status = nullptr;
+        uint8_t *d_in = nullptr, *d_out = nullptr;
         uint8_t* d_wire = nullptr;  // the chunk's wire image (zero-copy path)
-        uint32_t* d_len = nullptr;
-        // device addresses of the pinned blocks (the direct pipeline's kernels
-        // read and write them over the host link)
+        // device addresses of the pinned blocks: the kernels read lengths,
+        // nonces / AD and write statuses there over the host link, and the
+        // direct pipeline's kernels read and write the record staging there
         uint8_t *dh_in = nullptr, *dh_out = nullptr, *dh_meta = nullptr, *dh_status = nullptr;
         uint32_t* dh_len = nullptr;
         void* d_ws = nullptr;
@@ -251,9 +251,6 @@ void record_staging_free(RecordStaging* rs) {
         (void)hipFree(s.d_in);
         (void)hipFree(s.d_out);
         (void)hipFree(s.d_wire);
-        (void)hipFree(s.d_meta);
-        (void)hipFree(s.d_status);
-        (void)hipFree(s.d_len);
         (void)hipFree(s.d_ws);
         for (auto& e : s.ev)
             if (e) (void)hipEventDestroy(e);
@@ -289,9 +286,6 @@ int staging(sg_ctx* c, RecordStaging** out) {
             SG_HIP(hipMalloc((void**)&s.d_in, bytes));
             SG_HIP(hipMalloc((void**)&s.d_out, bytes));
             SG_HIP(hipMalloc((void**)&s.d_wire, bytes + 64));
-            SG_HIP(hipMalloc((void**)&s.d_meta, (size_t)kChunk * kMetaBytes));
-            SG_HIP(hipMalloc((void**)&s.d_status, kChunk));
-            SG_HIP(hipMalloc((void**)&s.d_len, kChunk * 4u));
             SG_HIP(hipMalloc(&s.d_ws, sg_workspace_size(kChunk)));
             for (auto& e : s.ev) SG_HIP(hipEventCreate(&e));
         }
@@ -545,7 +539,7 @@ inline void put_be64(uint8_t* p, uint64_t v) {
 // contiguous D2H; sg_read_records copies the chunk's wire image in, takes it
 // apart in HBM and copies the plaintext out contiguously.
 struct RegRange {
-    uintptr_t lo, hi;  // [lo, hi)
+    uintptr_t lo, hi, dev;  // [lo, hi) on the host; dev: its device address (hipHostGetDevicePointer)
 };
 std::mutex g_reg_mu;
 std::vector<RegRange> g_reg;
@@ -557,6 +551,35 @@ bool registered(const void* p, size_t n) {
         if (lo >= r.lo && hi <= r.hi) return true;
     return false;
 }
+// the device address of a byte of a registered range (nullptr if none)
+template <class T>
+T* reg_dev(T* p) {
+    const uintptr_t a = (uintptr_t)p;
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    for (const auto& r : g_reg)
+        if (a >= r.lo && a < r.hi) return (T*)(r.dev + (a - r.lo));
+    return nullptr;
+}
+
+// SG_RECORD_KD2H=1: zero-copy calls move their output by a kernel's stores
+// into the caller's registered memory over the host link (the write's frame
+// kernel builds the wire image straight in `wire`, the read's copy-out kernel
+// moves the plaintext into `out`), after the record kernels on the same
+// stream, instead of an SDMA D2H.  Round 6, same box (profiles/r06/
+// record_path_ab/, r06zz-r06zy): 28.1 / 25.5 GiB/s write / read both in a
+// standalone process and in the bench process, against SDMA's 21.6 / 21.0
+// standalone and 35.1 / 33.9 in the bench process (the SDMA copies' rate
+// depends on how the process's streams fall on the hardware queues; the
+// kernel's stores serialise with the record kernels of its stream).  The same
+// kernel on the D2H stream measured 21.7 / 21.4 and 25.9 / 23.9.  Default: SDMA.
+bool record_kd2h() {
+    static const bool on = [] {
+        const char* e = std::getenv("SG_RECORD_KD2H");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+
 // SG_ZERO_COPY=0 in the environment turns the registered-buffer path off (A/B)
 bool zero_copy_enabled() {
     static const bool on = [] {
@@ -580,10 +603,17 @@ size_t sg_wire_bound(size_t len) {
 
 int sg_host_register(void* p, size_t len) {
     if (!p || !len) return fail(SG_E_ARG, "NULL or empty range%s");
-    const hipError_t e = hipHostRegister(p, len, hipHostRegisterPortable);
+    // mapped: the zero-copy path's output kernels write the range over the
+    // host link (record_kd2h)
+    hipError_t e = hipHostRegister(p, len, hipHostRegisterPortable | hipHostRegisterMapped);
     if (e != hipSuccess) return sg::hip_fail(e, "hipHostRegister");
+    void* dev = nullptr;
+    if ((e = hipHostGetDevicePointer(&dev, p, 0)) != hipSuccess) {
+        (void)hipHostUnregister(p);
+        return sg::hip_fail(e, "hipHostGetDevicePointer");
+    }
     std::lock_guard<std::mutex> lk(sg::g_reg_mu);
-    sg::g_reg.push_back({(uintptr_t)p, (uintptr_t)p + len});
+    sg::g_reg.push_back({(uintptr_t)p, (uintptr_t)p + len, (uintptr_t)dev});
     return SG_OK;
 }
 
@@ -632,6 +662,9 @@ int64_t sg_write_records(sg_ctx* c, uint64_t seq0, uint8_t content_type, uint8_t
     // kernels read and write over the host link (the direct pipeline)
     const bool zc = zero_copy_enabled() && registered(data, len) && registered(wire, wire_need);
     const bool direct = record_direct() && !zc;
+    // zero-copy: the frame kernel writes the wire image into `wire` itself
+    // (its word stores need a 4-byte aligned wire)
+    const bool kd2h = zc && ((uintptr_t)wire & 3u) == 0 && record_kd2h();
     auto rec_len = [&](uint64_t r) { return (uint32_t)std::min<uint64_t>(SG_RECORD_MAX_LEN, len - r * SG_RECORD_MAX_LEN); };
     uint64_t next = 0;  // first record of the next chunk to stage
     SlotReset slot_reset(rs);
@@ -674,7 +707,6 @@ int64_t sg_write_records(sg_ctx* c, uint64_t seq0, uint8_t content_type, uint8_t
         } else {
             SG_HIP(hipMemcpyAsync(s.d_in, s.h_in, (size_t)k * kSlot, hipMemcpyHostToDevice, hs));
         }
-        if (!same) SG_HIP(hipMemcpyAsync(s.d_len, s.h_len, k * 4u, hipMemcpyHostToDevice, hs));
         SG_HIP(hipEventRecord(s.ev[1], hs));
         return SG_OK;
     };
@@ -702,7 +734,9 @@ int64_t sg_write_records(sg_ctx* c, uint64_t seq0, uint8_t content_type, uint8_t
         b.out = direct ? s.dh_out : s.d_out;
         b.out_stride = kSlot;
         // a uniform chunk is a direct launch; a ragged one (the tail) is bucketed
-        b.len = same ? nullptr : (direct ? s.dh_len : s.d_len);
+        // the lengths of a ragged chunk are read from the pinned block over the
+        // host link (a few hundred bytes: no copy of their own)
+        b.len = same ? nullptr : s.dh_len;
         b.uniform_len = same ? s.h_len[0] : 0u;
         b.max_len = SG_RECORD_MAX_LEN;
         b.stream = ks;
@@ -712,7 +746,8 @@ int64_t sg_write_records(sg_ctx* c, uint64_t seq0, uint8_t content_type, uint8_t
         if ((r = sg_seal_batch(&b)) != SG_OK) return r;
         if (s.zc) {
             const uint32_t hdr = content_type | ((uint32_t)ver_major << 8) | ((uint32_t)ver_minor << 16);
-            SG_HIP(launch_frame(s.d_out, kSlot, s.d_wire, (uint32_t)kWireRec, k, SG_RECORD_MAX_LEN + SG_MAC_LEN,
+            uint8_t* img = kd2h ? reg_dev(wire + s.first * kWireRec) : s.d_wire;
+            SG_HIP(launch_frame(s.d_out, kSlot, img, (uint32_t)kWireRec, k, SG_RECORD_MAX_LEN + SG_MAC_LEN,
                                 s.h_len[k - 1] + SG_MAC_LEN, hdr, ks));
         }
         SG_HIP(hipEventRecord(s.ev[2], ks));
@@ -720,6 +755,10 @@ int64_t sg_write_records(sg_ctx* c, uint64_t seq0, uint8_t content_type, uint8_t
     };
     auto copy_out = [&](RecordStaging::Slot& s) -> int {
         const uint32_t k = s.nrec, last = s.h_len[k - 1] + SG_MAC_LEN;
+        if (kd2h) {  // the frame kernel has written the wire already
+            SG_HIP(hipEventRecord(s.ev[3], streams(s).krn));
+            return SG_OK;
+        }
         const hipStream_t ds = streams(s).d2h;
         if (s.zc) {
             SG_HIP(hipMemcpyAsync(wire + s.first * kWireRec, s.d_wire, (size_t)(k - 1) * kWireRec + SG_HEADER_LEN + last,
@@ -792,6 +831,7 @@ int sg_read_records(sg_ctx* c, uint64_t seq0, const uint8_t* wire, size_t wire_l
     // the plaintext lengths, as if every record opens)
     const bool zc = zero_copy_enabled() && registered(wire, wire_len) && registered(out, need);
     const bool direct = record_direct() && !zc;
+    const bool kd2h = zc && record_kd2h();  // zero-copy chunks: a copy-out kernel writes `out`
     std::vector<uint64_t> pre;  // zc: plaintext offset of every record
     if (zc) {
         pre.resize(nrec + 1);
@@ -919,11 +959,6 @@ int sg_read_records(sg_ctx* c, uint64_t seq0, const uint8_t* wire, size_t wire_l
                                   hipMemcpyHostToDevice, hs));
         } else {
             SG_HIP(hipMemcpyAsync(s.d_in, s.h_in, (size_t)k * kSlot, hipMemcpyHostToDevice, hs));
-            if (!same) SG_HIP(hipMemcpyAsync(s.d_len, s.h_len, k * 4u, hipMemcpyHostToDevice, hs));
-        }
-        if (!tls) {
-            SG_HIP(hipMemcpyAsync(s.d_meta, s.h_meta, 8u * k, hipMemcpyHostToDevice, hs));
-            SG_HIP(hipMemcpyAsync(s.d_meta + 8u * kChunk, s.h_meta + 8u * kChunk, 13u * k, hipMemcpyHostToDevice, hs));
         }
         SG_HIP(hipEventRecord(s.ev[1], hs));
         s.nrec = k;
@@ -954,7 +989,7 @@ int sg_read_records(sg_ctx* c, uint64_t seq0, const uint8_t* wire, size_t wire_l
             b.ver_major = R0.major;
             b.ver_minor = R0.minor;
         } else {
-            uint8_t* meta = direct ? s.dh_meta : s.d_meta;
+            uint8_t* meta = s.dh_meta;  // (read over the host link, no copy of its own)
             b.nonces = meta;
             b.ads = meta + 8u * kChunk;
             b.ad_len = 13;
@@ -966,10 +1001,13 @@ int sg_read_records(sg_ctx* c, uint64_t seq0, const uint8_t* wire, size_t wire_l
         b.out = direct ? s.dh_out : s.d_out;
         // zero-copy: plaintext back to back, as it lands in `out`
         b.out_stride = s.zc ? (size_t)(R0.flen - SG_MAC_LEN) : kSlot;
-        b.len = same ? nullptr : (direct ? s.dh_len : s.d_len);
+        // lengths, nonces / AD and the per-record status go over the host link
+        // in the kernels' own accesses, not in copies of their own (round 6:
+        // one small D2H per chunk fewer on the copy engine)
+        b.len = same ? nullptr : s.dh_len;
         b.uniform_len = same ? R0.flen : 0u;
         b.max_len = SG_ENC_RECORD_MAX_LEN;
-        b.status = direct ? s.dh_status : s.d_status;
+        b.status = s.dh_status;
         b.stream = ks;
         b.workspace = s.d_ws;
         b.workspace_size = sg_workspace_size(kChunk);
@@ -980,11 +1018,17 @@ int sg_read_records(sg_ctx* c, uint64_t seq0, const uint8_t* wire, size_t wire_l
         if (!s.zc) b.flags |= SG_BATCH_KEEP_FAILED;
         int r;
         if ((r = sg_open_batch(&b)) != SG_OK) return r;
+        if (s.zc && kd2h)
+            SG_HIP(launch_copy_out(s.d_out, reg_dev(out + pre[s.first]), pre[s.first + k] - pre[s.first], ks));
         SG_HIP(hipEventRecord(s.ev[2], ks));
         return SG_OK;
     };
     auto copy_out = [&](RecordStaging::Slot& s) -> int {
         const uint32_t k = s.nrec;
+        if (s.zc && kd2h) {  // the copy-out kernel has written `out` already
+            SG_HIP(hipEventRecord(s.ev[3], streams(s).krn));
+            return SG_OK;
+        }
         const hipStream_t ds = streams(s).d2h;
         if (s.zc) {
             SG_HIP(hipMemcpyAsync(out + pre[s.first], s.d_out, pre[s.first + k] - pre[s.first], hipMemcpyDeviceToHost,
@@ -992,7 +1036,6 @@ int sg_read_records(sg_ctx* c, uint64_t seq0, const uint8_t* wire, size_t wire_l
         } else {
             SG_HIP(hipMemcpyAsync(s.h_out, s.d_out, (size_t)k * kSlot, hipMemcpyDeviceToHost, ds));
         }
-        SG_HIP(hipMemcpyAsync(s.h_status, s.d_status, k, hipMemcpyDeviceToHost, ds));
         SG_HIP(hipEventRecord(s.ev[3], ds));
         return SG_OK;
     };
