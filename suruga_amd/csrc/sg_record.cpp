@@ -216,6 +216,31 @@ bool record_direct() {
     }();
     return on;
 }
+// The direct pipeline's kernel stream of each context is created at the
+// device's greatest stream priority: such streams draw their hardware queues
+// from a pool of their own, which the process's other streams do not share,
+// so a writer's and a reader's record kernels never queue behind each other or
+// behind unrelated work (round 6, profiles/r06/record_path_ab/r06ps: pageable
+// 22.1 / 22.2 and 20.7 / 21.6 GiB/s in the bench process against 19.8 / 20.2
+// and 19.5 / 19.3, duplex standalone 28.5 / 28.2 against 25.2 / 25.0; one
+// earlier default-priority run of the bench process ran the duplex at 0.91x
+// the serial time, r06pr).  The same for the copy-engine pipeline's copy or
+// kernel streams slowed the registered path (34.9 -> 26-27 GiB/s, r06pr), so
+// those stay at the default priority.  SG_DIRECT_PRIO=0: default priority (A/B).
+bool direct_stream_high() {
+    static const bool on = [] {
+        const char* e = std::getenv("SG_DIRECT_PRIO");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+hipError_t make_stream(hipStream_t* s, bool high) {
+    if (!high) return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+    int least = 0, greatest = 0;
+    hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+    if (e != hipSuccess) return e;
+    return hipStreamCreateWithPriority(s, hipStreamNonBlocking, greatest);
+}
 std::mutex g_cs_mu;
 std::vector<std::pair<int, std::pair<hipStream_t, hipStream_t>>> g_copy_streams;  // device -> (h2d, d2h)
 hipError_t process_copy_streams(int dev, hipStream_t* h2d, hipStream_t* d2h) {
@@ -349,7 +374,7 @@ struct SlotReset {
 // the streams of slot i for this call (mode: copy_streams_mode)
 int pipe_streams(sg_ctx* c, RecordStaging* rs, int i, bool direct, PipeStreams* out) {
     if (direct) {
-        if (!rs->kst) SG_HIP(hipStreamCreateWithFlags(&rs->kst, hipStreamNonBlocking));
+        if (!rs->kst) SG_HIP(make_stream(&rs->kst, direct_stream_high()));
         *out = {rs->kst, rs->kst, rs->kst};
         return SG_OK;
     }

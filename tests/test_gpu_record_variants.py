@@ -12,7 +12,8 @@ per-direction + duplex record-path check in a child process of its own:
 * SG_RECORD_KD2H=1: zero-copy output by kernel stores instead of an SDMA D2H;
 * SG_COPY_STREAMS=0 SG_RECORD_SLOTS=2: per-slot streams, the shallowest
   pipeline;
-* SG_ZERO_COPY=0: registered buffers through the staged path.
+* SG_ZERO_COPY=0: registered buffers through the staged path;
+* SG_DIRECT_PRIO=0: the direct pipeline's kernel streams at default priority.
 """
 from __future__ import annotations
 
@@ -33,6 +34,7 @@ VARIANTS = {
     "kd2h": {"SG_RECORD_KD2H": "1"},
     "slot_streams": {"SG_COPY_STREAMS": "0", "SG_RECORD_SLOTS": "2"},
     "no_zero_copy": {"SG_ZERO_COPY": "0"},
+    "direct_default_prio": {"SG_DIRECT_PRIO": "0"},
 }
 
 
