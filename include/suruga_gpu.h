@@ -197,12 +197,14 @@ int sg_open_batch(const sg_batch* b);
 
 /* ---- batched record layer over host memory ------------------------------
  * The throughput form of TlsWriter / TlsReader (tls.rs:68-380): many records
- * per call, pipelined host<->device copies inside the library (four chunks
- * of 256 records in flight: coming in, in the kernels, going out; each step
+ * per call, pipelined inside the library, up to four chunks of 256 records in
+ * flight.  Unregistered (pageable) buffers: the records are framed through
+ * pinned staging that the kernels read and write over the host link
+ * themselves.  Registered buffers (sg_host_register): host<->device copies
+ * straight from and into them, each step (copy in, kernels, copy out)
  * enqueued by the calling thread once the step before it has completed, so
  * that a reader and a writer on two contexts never queue behind each other's
- * unfinished work; pinned staging for unregistered buffers), wire format exactly as the
- * reference writes and parses it:
+ * unfinished work.  Wire format exactly as the reference writes and parses it:
  *   header = content_type || major || minor || be16(fragment length)
  *   (tls.rs:126-130, 218-236) followed by the fragment (ct || tag).        */
 #define SG_RECORD_MAX_LEN      16384u              /* RECORD_MAX_LEN      tls.rs:32 */
@@ -280,7 +282,9 @@ int sg_parse_records(const uint8_t* wire, size_t wire_len, size_t max_records, s
 
 /* Time (ms) spent by the last sg_write_records / sg_read_records call of this
  * thread in host->device copies, kernels and device->host copies (HIP events;
- * summed over the pipelined chunks) and in host-side framing memcpy. */
+ * summed over the pipelined chunks; with unregistered buffers the kernels move
+ * the bytes over the host link themselves and all device time counts as
+ * kernels) and in host-side framing memcpy. */
 int sg_record_timing(double* h2d_ms, double* kernel_ms, double* d2h_ms, double* host_ms);
 
 /* ---- TLS 1.2 key schedule on the host (cipher/prf.rs, client.rs:130-225) --

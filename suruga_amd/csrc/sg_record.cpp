@@ -2,13 +2,17 @@
 // sg_read_records): the throughput form of suruga's TlsWriter::write_data and
 // TlsReader::read_record (src/tls.rs:99-147, 217-281).
 //
-// Records move through a per-context pipeline of three slots.  Each slot owns
-// device buffers, a keying workspace and (staged path, allocated on first use)
-// pinned host buffers; while the GPU seals/opens chunk c on one slot, chunk
-// c-1's output leaves and chunk c+1 comes in on the others.  Device layout is
-// always 16-byte aligned (record slot stride kSlot), so the kernels take their
-// vector path; the 5-byte TLS headers are added/stripped by the CPU while
-// copying (staged path) or by the frame kernels in HBM (zero-copy path).
+// Records move through a per-context pipeline of four slots (record_slots).
+// Each slot owns device buffers, a keying workspace and (staged path,
+// allocated on first use) pinned host buffers.  Staged calls run the direct
+// pipeline (run_direct): the host frames chunk c+1 into a slot's pinned
+// staging while the kernels of chunk c read and write another slot's staging
+// over the host link.  Zero-copy calls (sg_host_register'ed buffers) run the
+// copy-engine pipeline (run_pipeline): while the GPU seals/opens chunk c, chunk
+// c-1's output leaves and chunk c+1 comes in.  Device layout is always 16-byte
+// aligned (record slot stride kSlot), so the kernels take their vector path;
+// the 5-byte TLS headers are added/stripped by the CPU while copying (staged
+// path) or by the frame kernels in HBM (zero-copy path).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -54,7 +58,10 @@ double now_ms() {
 // reader and a writer thread) each queue a job and the workers take indices
 // from the oldest job that still has some, so both progress.
 // SG_COPY_THREADS sets the total (default 8: tools/record_path_bench.py
-// measured 9.8 / 11.5 / 15.5 / 15.2 GiB/s per direction with 1 / 4 / 8 / 16).
+// measured 9.8 / 11.5 / 15.5 / 15.2 GiB/s per direction with 1 / 4 / 8 / 16
+// in round 4; with round 6's direct pipeline 20.7 / 22.6 / 19.4 / 20.0 GiB/s
+// write with 8 / 12 / 16 / 24, profiles/r06/record_path_ab/threads_r06.json:
+// the host's memory, not the thread count, bounds it).
 class CopyPool {
   public:
     static CopyPool& shared() {
