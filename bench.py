@@ -351,18 +351,20 @@ def measure_record_path(args, bus):
         return True
 
     total = args.record_path_bytes
-    data = np.frombuffer(np.random.default_rng(0xC4).bytes(total), dtype=np.uint8).copy()
     runs = {}
     t0 = time.perf_counter()
-    for reg in (False, True):
-        runs["registered" if reg else "pageable"] = one(total, 64 << 20, 0, reg, check_wire, data)
+    try:
+        data = np.frombuffer(np.random.default_rng(0xC4).bytes(total), dtype=np.uint8).copy()
+        for reg in (False, True):
+            runs["registered" if reg else "pageable"] = one(total, 64 << 20, 0, reg, check_wire, data)
+    finally:  # the timed C1 / C2 work before ran unpinned; so does whatever follows
+        os.sched_setaffinity(0, prev)
     out = {"bytes": total, "call_bytes": 64 << 20, "copy_threads": int(os.environ.get("SG_COPY_THREADS", "8")),
            "note": "application GiB/s per direction from host memory, every copy inside; duplex.gibs counts both "
                    "directions' bytes; one key, seq from 0, content type 23, TLS 1.2 (tls.rs:126-130, 238-281)",
            **runs, "wall_s": round(time.perf_counter() - t0, 1)}
     out["correct"] = all(r["correct"] and r["duplex"]["correct"] and r["wire_sample_ok"] for r in runs.values())
     out["pinned"] = {"cpus": len(cpus) if cpus else None, "how": how}
-    os.sched_setaffinity(0, prev)
     return out
 
 
