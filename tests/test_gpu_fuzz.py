@@ -125,3 +125,20 @@ def test_random_mixed_batches(gpu, oracle, seed):
             assert back_h[o:o + n] == pt_h[o:o + n], (seed, i, n)
         elif exp_st[i] == 1 and not keep:
             assert back_h[o:o + n] == bytes(n), (seed, i, n)  # nothing of a failed record is released
+
+
+@pytest.mark.parametrize("lockstep,packed", [(0, 0), (0, 1), (1, 0)])
+@pytest.mark.parametrize("seed", [11, 12, 13, 14])
+def test_random_mixed_batches_every_kernel_form(gpu, oracle, seed, lockstep, packed):
+    """The same random batches with the wave-per-record kernel and / or the
+    packed kernel switched off (sg_set_lockstep / sg_set_packed): every record
+    then runs on another route (size classes), bit-exact all the same."""
+    from suruga_amd import _native
+
+    lib = _native.load()
+    prev_l, prev_p = lib.sg_set_lockstep(lockstep), lib.sg_set_packed(packed)
+    try:
+        test_random_mixed_batches(gpu, oracle, seed)
+    finally:
+        lib.sg_set_lockstep(prev_l)
+        lib.sg_set_packed(prev_p)
